@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Benchmark: MI355X FLAC frame decode on BASELINE config C2 (one JSON line on rank 0).
+
+Workload: batches of 1024 synthetic frames (44.1 kHz / 16-bit stereo, blocksize 4096,
+LPC order 8, Rice partition order 4), the compressed frames resident in HBM.  One step
+decodes ``--batches`` independent batches (distinct copies in HBM, so nothing is served
+from a previous step's cache footprint) into FLACDecoder's 16-bit interleaved LE PCM
+(the OpenAL buffer-fill layout, FLACDecoder.cs:543-562) with the two kernels of the
+path, k_parse and k_decode, on one HIP stream.
+
+value      = decoded samples (blocksize x channels) per second,
+             whole job over all ranks (weak scaling: every rank decodes its own batches).
+roofline   = the dominant kernel (k_decode): algorithmic bytes (compressed frame bytes +
+             PCM bytes written) / its HIP-event-timed average duration, vs 8 TB/s HBM.
+cpu_baseline = the CPU restatement (oracle/: libFLAC 1.2.1 decode + FLACDecoder pack),
+             one thread, on a bounded sample of the same frames.
+
+    python bench.py [--gpus N --steps K --warmup W --batches B]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "decoded PCM MSamples/s/GPU (bit-exact) + achieved HBM GB/s vs roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batches", type=int, default=64, help="C2 batches (x1024 frames) decoded per step")
+    ap.add_argument("--frames", type=int, default=1024, help="frames per batch (BASELINE C2: 1024)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--out", default=None, help="also write the JSON line here")
+    return ap.parse_args()
+
+
+def cpu_baseline(data: bytes, nsamples_per_pass: int, budget_s: float):
+    """Oracle (restated libFLAC 1.2.1 + FLACDecoder.CopyTo pack), single thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.lib()
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        rc, pk, msg, _ = oracle.flacdecoder_copyto(data)
+        assert rc == 0, msg
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return passes * nsamples_per_pass / el / 1e6, passes, el
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    from birdnest.audio_amd import libflac, synth
+    p = synth.config("C2", nframes=args.frames, seed=2)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    offs = s.frame_offsets.astype(np.int64)
+    fb_in = int(len(data) - offs[0])               # compressed frame bytes (sync .. CRC-16)
+    samples_per_batch = int(s.nsamples) * p.channels
+    sp = libflac.StreamParams.from_synth(p, s.nsamples)
+    stride = libflac.out_stride(libflac.OUT_FLACDECODER, sp)
+    pcm_bytes_per_batch = int(s.nsamples) * stride
+    B = args.batches
+
+    # B distinct copies of the batch in HBM (4-byte aligned), one output region each
+    copy_len = (len(data) + 255) // 256 * 256
+    host = np.zeros(copy_len * B + 64, dtype=np.uint8)
+    src = np.frombuffer(data, dtype=np.uint8)
+    for b in range(B):
+        host[b * copy_len: b * copy_len + len(data)] = src
+    d_bytes = torch.from_numpy(host).to(dev)
+    nbytes_total = copy_len * B
+    d_offs = torch.from_numpy(np.concatenate([offs + b * copy_len for b in range(B)])).to(dev)
+    nframes = args.frames * B
+    fr_bs = np.full(args.frames, p.blocksize, dtype=np.int64)
+    fr_start = np.concatenate([[0], np.cumsum(fr_bs)[:-1]])
+    d_out_sample = torch.from_numpy(np.concatenate([fr_start + b * int(s.nsamples) for b in range(B)])).to(dev)
+    d_out = torch.empty(pcm_bytes_per_batch * B, dtype=torch.uint8, device=dev)
+    d_info = torch.zeros(nframes * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    dec = libflac.BatchDecoder(local_rank)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        dec.parse_frames(d_bytes, nbytes_total, d_offs, nframes, sp, d_info, d_out_sample=d_out_sample, stream=stream)
+        if evs is not None:
+            evs[1].record(stream)
+        dec.decode_parsed(d_bytes, nbytes_total, nframes, sp, libflac.OUT_FLACDECODER, d_out, d_info, stream=stream)
+        if evs is not None:
+            evs[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_parse = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps  # ms
+    t_decode = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness of what was timed: every frame ok, copies 0 and B-1 == source PCM
+    info = libflac.info_array(d_info.view(-1, libflac.FRAME_INFO_BYTES)[:: max(1, nframes // 4096)].cpu().numpy())
+    ok = bool((info["status"] == 0).all() and (info["crc_ok"] == 1).all())
+    ref = s.pcm.astype("<i2").tobytes()
+    for b in {0, B - 1}:
+        got = d_out[b * pcm_bytes_per_batch:(b + 1) * pcm_bytes_per_batch].cpu().numpy().tobytes()
+        ok = ok and got == ref
+    if world > 1:
+        o = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(o, op=dist.ReduceOp.MIN)
+        ok = bool(o.item())
+
+    total_samples = samples_per_batch * B * args.steps * world
+    value = total_samples / elapsed / 1e6
+    alg_bytes = (fb_in + pcm_bytes_per_batch) * B
+    achieved = alg_bytes / (t_decode * 1e-3) / 1e9
+    step_achieved = alg_bytes / ((t_parse + t_decode) * 1e-3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "MSamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic: deterministic generator (seed 2), BASELINE C2 frame shape",
+        "config": {"workload": "C2: 1024-frame batches, 44.1 kHz/16-bit stereo, bs 4096, LPC-8, Rice partition "
+                               "order 4 -> FLACDecoder 16-bit LE interleaved PCM",
+                   "frames_per_batch": args.frames, "batches_per_step": B,
+                   "compressed_bytes_per_batch": fb_in, "pcm_bytes_per_batch": pcm_bytes_per_batch,
+                   "parallelism": f"frames sharded per rank x{world}"},
+        "bitexact": ok,
+        "roofline": {"bound": "hbm", "kernel": "k_decode", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(t_decode, 4),
+                     "k_parse_avg_ms": round(t_parse, 4), "step_achieved_GBs": round(step_achieved, 1)},
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        sys.stdout.flush()
+        mss, passes, el = cpu_baseline(data, samples_per_batch, args.cpu_seconds)
+        line["cpu_baseline"] = {"value": round(mss, 3), "unit": "MSamples/s", "cores": 1, "kind": "port",
+                                "sample": f"{passes} x one C2 batch ({args.frames} frames, {samples_per_batch} samples) "
+                                          f"through the oracle's FLACDecoder.CopyTo replay, {el:.1f} s"}
+    if rank == 0:
+        js = json.dumps(line)
+        print(js, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(js + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,73 @@
+"""Build the in-tree native libraries (hipcc for gfx950, gcc for host-only C).
+
+    libbnflac.so        -- HIP kernels + C ABI (the product)
+    libbnflac_synth.so  -- synthetic FLAC workload generator
+
+Outputs go to birdnest/audio_amd/lib/ so they travel with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(PKG))
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib")
+INCLUDE = os.path.join(ROOT, "include")
+
+HIP_SOURCES = [os.path.join(CSRC, "bnflac_kernels.hip"), os.path.join(CSRC, "bnflac_runtime.cpp")]
+HIP_HEADERS = [os.path.join(CSRC, "bnflac_device.h"), os.path.join(INCLUDE, "bnflac.h"),
+               os.path.join(INCLUDE, "FLAC_compat.h")]
+SYNTH_SOURCES = [os.path.join(CSRC, "synth", "bnflac_synth.c")]
+SYNTH_HEADERS = [os.path.join(CSRC, "synth", "bnflac_synth.h")]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def build_hip(force=False, verbose=False):
+    out = os.path.join(LIB, "libbnflac.so")
+    if force or _stale(out, HIP_SOURCES + HIP_HEADERS):
+        os.makedirs(LIB, exist_ok=True)
+        cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+               "-I" + INCLUDE] + HIP_SOURCES + ["-o", out + ".tmp"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def build_synth(force=False, verbose=False):
+    out = os.path.join(LIB, "libbnflac_synth.so")
+    if force or _stale(out, SYNTH_SOURCES + SYNTH_HEADERS):
+        os.makedirs(LIB, exist_ok=True)
+        cmd = ["gcc", "-O2", "-fPIC", "-shared", "-Wall"] + SYNTH_SOURCES + ["-o", out + ".tmp", "-lm"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def build_all(force=False, verbose=False):
+    return [build_synth(force, verbose), build_hip(force, verbose)]
+
+
+if __name__ == "__main__":
+    for p in build_all(force="--force" in sys.argv, verbose=True):
+        print(p)

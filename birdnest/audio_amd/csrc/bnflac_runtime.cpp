@@ -1,0 +1,1054 @@
+/*
+ * bnflac_runtime.cpp -- host side of libbnflac.so.
+ *
+ *  - bnflac_* batched API: thin, asynchronous launchers over the HIP kernels.
+ *  - FLAC__stream_decoder_*: libFLAC 1.2.1-compatible stream decoder.  Metadata and
+ *    the libFLAC state machine (find_metadata_, frame_sync_, the per-frame error and
+ *    write sequence of read_frame_, LibFlac.dll@0x10010130/0x10011760/0x100118c0) are
+ *    replayed on the host from per-frame records; every frame body is decoded on the
+ *    GPU in windows of many frames at once.  Read-ahead changes when the client's read
+ *    callback is called, never what the write/error callbacks receive.
+ *
+ * The product path has no CPU decode: if no GPU is usable the decoder fails loudly
+ * (init returns MEMORY_ALLOCATION_ERROR and bnflac_last_error() says why).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <sys/stat.h>
+#include <vector>
+
+#include "../../../include/bnflac.h"
+#include "bnflac_device.h"
+
+static_assert(sizeof(bnflac_frame_info) == sizeof(bnf_frame_info), "frame info layout");
+static_assert(sizeof(bnf_frame_info) == 128, "frame info is 128 bytes");
+static_assert(offsetof(FLAC__FrameHeader, number) == 24, "FrameHeader.FrameOrSampleNumber @24 (LibFLACSharp.cs:232)");
+static_assert(offsetof(FLAC__FrameHeader, crc) == 32, "FrameHeader.Crc @32 (LibFLACSharp.cs:233)");
+static_assert(offsetof(FLAC__StreamMetadata, data) == 16, "StreamMetadata.data @16 (LibFLACSharp.cs:299)");
+static_assert(offsetof(FLAC__StreamMetadata, data.stream_info.sample_rate) == 32, "sample_rate @32");
+static_assert(offsetof(FLAC__StreamMetadata, data.stream_info.total_samples) == 48, "total_samples @48");
+
+extern "C" {
+hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow);
+hipError_t bnf_launch_sync_scan(const uint8_t *d, uint64_t n, uint32_t *d_block_counts, uint32_t *d_total,
+                                uint64_t *d_out, uint32_t cap, hipStream_t s);
+uint32_t bnf_scan_blocks(uint64_t n);
+hipError_t bnf_launch_parse(const uint32_t *words, uint32_t nwords, uint64_t nbytes, const uint64_t *frame_offs,
+                            uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
+                            uint64_t base_sample, bnf_frame_info *info, hipStream_t s);
+hipError_t bnf_launch_decode(const uint32_t *words, uint32_t nwords, uint64_t nbytes, uint32_t nframes,
+                             bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
+                             bnf_frame_info *info, hipStream_t s);
+}
+
+/* ------------------------------------------------------------------ errors */
+static thread_local std::string g_err;
+static int fail(const std::string &m, int code = -1) {
+    g_err = m;
+    return code;
+}
+extern "C" BNFLAC_API const char *bnflac_last_error(void) { return g_err.c_str(); }
+
+/* ------------------------------------------------------------ CRC tables */
+static void build_tables(uint8_t *c8, uint16_t *c16, uint16_t *xp) {
+    for (int i = 0; i < 256; i++) {
+        uint8_t c = (uint8_t)i;
+        for (int b = 0; b < 8; b++) c = (uint8_t)((c & 0x80) ? (c << 1) ^ 0x07 : (c << 1));
+        c8[i] = c;
+        uint16_t w = (uint16_t)(i << 8);
+        for (int b = 0; b < 8; b++) w = (uint16_t)((w & 0x8000) ? (w << 1) ^ 0x8005 : (w << 1));
+        c16[i] = w;
+    }
+    for (int k = 1; k < 8; k++)
+        for (int i = 0; i < 256; i++) {
+            uint16_t p = c16[(k - 1) * 256 + i];
+            c16[k * 256 + i] = (uint16_t)((p << 8) ^ c16[p >> 8]);
+        }
+    /* x^(8*2^j) mod P */
+    auto mulmod = [](uint32_t a, uint32_t b) {
+        uint32_t r = 0;
+        for (int i = 15; i >= 0; i--) {
+            r = (r & 0x8000u) ? ((r << 1) ^ 0x8005u) & 0xffffu : (r << 1);
+            if ((b >> i) & 1u) r ^= a;
+        }
+        return r;
+    };
+    uint32_t v = 0x0100; /* x^8 */
+    for (int j = 0; j < 40; j++) {
+        xp[j] = (uint16_t)v;
+        v = mulmod(v, v);
+    }
+}
+
+static std::mutex g_dev_mu;
+static bool g_tables_ready[64];
+
+static int ensure_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail("bnflac: no HIP device available (the decode path is GPU-only)");
+    if (dev < 0 || dev >= n || dev >= 64) return fail("bnflac: bad device index");
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (hipSetDevice(dev) != hipSuccess) return fail("bnflac: hipSetDevice failed");
+    if (!g_tables_ready[dev]) {
+        uint8_t c8[256];
+        uint16_t c16[8 * 256], xp[40];
+        build_tables(c8, c16, xp);
+        if (bnf_upload_tables(c8, c16, xp) != hipSuccess) return fail("bnflac: table upload failed");
+        g_tables_ready[dev] = true;
+    }
+    return 0;
+}
+
+extern "C" BNFLAC_API int bnflac_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+/* ----------------------------------------------------------------- context */
+struct bnflac_ctx {
+    int device;
+    uint32_t *d_block_counts = nullptr;
+    uint32_t block_cap = 0;
+};
+
+extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
+    *out = nullptr;
+    if (ensure_device(device)) return -1;
+    bnflac_ctx *c = new bnflac_ctx();
+    c->device = device;
+    *out = c;
+    return 0;
+}
+
+extern "C" BNFLAC_API void bnflac_ctx_destroy(bnflac_ctx *ctx) {
+    if (!ctx) return;
+    if (ctx->d_block_counts) (void)hipFree(ctx->d_block_counts);
+    delete ctx;
+}
+
+static uint32_t lanes_for(uint32_t channels) {
+    uint32_t l = 1;
+    while (l < channels) l <<= 1;
+    return l > 8 ? 8 : l;
+}
+
+extern "C" BNFLAC_API uint32_t bnflac_out_stride(int fmt, const bnflac_stream_params *sp) {
+    switch (fmt) {
+    case BNFLAC_OUT_PLANAR32:
+    case BNFLAC_OUT_INTERLEAVED32: return 4u * sp->channels;
+    case BNFLAC_OUT_FLACDECODER: return sp->channels == 2 ? 4u : 2u;
+    default: return sp->channels * (sp->bps == 24 ? 3u : 2u);
+    }
+}
+
+extern "C" BNFLAC_API int bnflac_index_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
+                                              uint64_t *d_offsets, uint32_t cap, uint32_t *d_count, void *hs) {
+    if (!ctx) return fail("bnflac_index_frames: null ctx");
+    if (((uintptr_t)d_bytes) & 3u) return fail("bnflac_index_frames: d_bytes must be 4-byte aligned");
+    const uint32_t nb = bnf_scan_blocks(nbytes);
+    if (nb > ctx->block_cap) {
+        if (ctx->d_block_counts) (void)hipFree(ctx->d_block_counts);
+        ctx->d_block_counts = nullptr;
+        if (hipMalloc(&ctx->d_block_counts, sizeof(uint32_t) * (size_t)std::max(nb, 1u)) != hipSuccess)
+            return fail("bnflac_index_frames: out of device memory");
+        ctx->block_cap = nb;
+    }
+    hipError_t e = bnf_launch_sync_scan(d_bytes, nbytes, ctx->d_block_counts, d_count, d_offsets, cap, (hipStream_t)hs);
+    return e == hipSuccess ? 0 : fail(std::string("bnflac_index_frames: ") + hipGetErrorString(e));
+}
+
+static int check_args(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, const bnflac_stream_params *sp,
+                      const char *who) {
+    if (!ctx || !sp) return fail(std::string(who) + ": null argument");
+    if (((uintptr_t)d_bytes) & 3u) return fail(std::string(who) + ": d_bytes must be 4-byte aligned");
+    if (sp->channels < 1 || sp->channels > 8) return fail(std::string(who) + ": channels must be 1..8");
+    if (nbytes >= (1ull << 34)) return fail(std::string(who) + ": buffer larger than 16 GiB");
+    return 0;
+}
+
+extern "C" BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
+                                              const uint64_t *d_frame_offsets, uint32_t nframes,
+                                              const bnflac_stream_params *sp, const uint64_t *d_out_sample,
+                                              uint64_t base_sample, bnflac_frame_info *d_info, void *hs) {
+    if (check_args(ctx, d_bytes, nbytes, sp, "bnflac_parse_frames")) return -1;
+    bnf_stream_params p;
+    memcpy(&p, sp, sizeof p);
+    hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, (uint32_t)((nbytes + 3) / 4), nbytes, d_frame_offsets,
+                                    nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info, (hipStream_t)hs);
+    return e == hipSuccess ? 0 : fail(std::string("k_parse: ") + hipGetErrorString(e));
+}
+
+extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, uint32_t nframes,
+                                               const bnflac_stream_params *sp, int out_format, uint8_t *d_out,
+                                               uint64_t out_bytes, bnflac_frame_info *d_info, void *hs) {
+    if (check_args(ctx, d_bytes, nbytes, sp, "bnflac_decode_parsed")) return -1;
+    if (out_format < 0 || out_format > 3) return fail("bnflac_decode_parsed: bad out_format");
+    bnf_stream_params p;
+    memcpy(&p, sp, sizeof p);
+    hipError_t e = bnf_launch_decode((const uint32_t *)d_bytes, (uint32_t)((nbytes + 3) / 4), nbytes, nframes, p,
+                                     lanes_for(sp->channels), out_format, d_out, out_bytes, (bnf_frame_info *)d_info,
+                                     (hipStream_t)hs);
+    return e == hipSuccess ? 0 : fail(std::string("k_decode: ") + hipGetErrorString(e));
+}
+
+extern "C" BNFLAC_API int bnflac_decode_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
+                                               const uint64_t *d_frame_offsets, uint32_t nframes,
+                                               const bnflac_stream_params *sp, const uint64_t *d_out_sample,
+                                               uint64_t base_sample, int out_format, uint8_t *d_out, uint64_t out_bytes,
+                                               bnflac_frame_info *d_info, void *hs) {
+    if (out_format < 0 || out_format > 3) return fail("bnflac_decode_frames: bad out_format");
+    int rc = bnflac_parse_frames(ctx, d_bytes, nbytes, d_frame_offsets, nframes, sp, d_out_sample, base_sample, d_info, hs);
+    if (rc) return rc;
+    return bnflac_decode_parsed(ctx, d_bytes, nbytes, nframes, sp, out_format, d_out, out_bytes, d_info, hs);
+}
+
+/* ====================================================================== */
+/*                 libFLAC-compatible stream decoder                       */
+/* ====================================================================== */
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    bool grow(size_t n) {
+        if (n <= cap) return true;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = std::max<size_t>(n, 1 << 16);
+        c = c + c / 4;
+        if (hipMalloc(&p, c) != hipSuccess) return false;
+        cap = c;
+        return true;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+} // namespace
+
+struct FLAC__StreamDecoder {
+    FLAC__StreamDecoderState state = FLAC__STREAM_DECODER_UNINITIALIZED;
+    FLAC__StreamDecoderReadCallback read_cb = nullptr;
+    FLAC__StreamDecoderSeekCallback seek_cb = nullptr;
+    FLAC__StreamDecoderTellCallback tell_cb = nullptr;
+    FLAC__StreamDecoderLengthCallback length_cb = nullptr;
+    FLAC__StreamDecoderEofCallback eof_cb = nullptr;
+    FLAC__StreamDecoderWriteCallback write_cb = nullptr;
+    FLAC__StreamDecoderMetadataCallback metadata_cb = nullptr;
+    FLAC__StreamDecoderErrorCallback error_cb = nullptr;
+    void *client = nullptr;
+    FILE *file = nullptr;
+    bool ignore_write_status = false;
+
+    /* every byte delivered by the read callback; pos = consumed */
+    std::vector<uint8_t> buf;
+    uint64_t pos = 0;
+    uint64_t bitpos_meta = 0; /* bit cursor used while reading metadata */
+    bool cached = false;
+    uint8_t lookahead = 0;
+    uint8_t header_warmup[2] = {0, 0};
+    int client_done = 0; /* 1: client reported end of stream, 2: abort */
+
+    bool has_stream_info = false;
+    FLAC__StreamMetadata stream_info;
+    uint64_t samples_decoded = 0;
+    unsigned fixed_block_size = 0, next_fixed_block_size = 0;
+    uint64_t first_frame_offset = 0;
+    bool is_seeking = false;
+    uint64_t seek_target = 0;
+    int seek_done = 0;
+
+    FLAC__Frame frame;
+    std::vector<int32_t> output[FLAC__MAX_CHANNELS];
+    unsigned output_capacity = 0, output_channels = 0;
+
+    unsigned channels = 0, bits_per_sample = 0, sample_rate = 0, blocksize = 0;
+    FLAC__ChannelAssignment channel_assignment = FLAC__CHANNEL_ASSIGNMENT_INDEPENDENT;
+
+    /* GPU window */
+    int device = 0;
+    bool gpu_ready = false;
+    hipStream_t stream = nullptr;
+    bnflac_ctx *ctx = nullptr;
+    DevBuf d_bytes, d_cand, d_count, d_info, d_pcm;
+    uint64_t win_base = 0, win_end = 0;
+    bool win_valid = false;
+    std::vector<uint64_t> cand;
+    std::vector<bnf_frame_info> info;
+    std::vector<int32_t> pcm;
+    uint64_t read_ahead = 32ull << 20;
+};
+
+namespace {
+
+using Dec = FLAC__StreamDecoder;
+
+/* read_callback_ (stream_decoder.c) semantics, without touching the decoder state:
+ * 0 = got bytes, 1 = end of stream, 2 = abort. */
+int fill_raw(Dec *d, size_t want = 65536) {
+    if (d->client_done) {
+        /* libFLAC would ask again: the eof callback answers first */
+        if (d->client_done == 2) return 2;
+        if (d->eof_cb && d->eof_cb(d, d->client)) return 1;
+    }
+    for (int spins = 0; spins < 1000000; spins++) {
+        if (d->eof_cb && d->eof_cb(d, d->client)) return 1;
+        size_t old = d->buf.size();
+        size_t bytes = want;
+        d->buf.resize(old + bytes);
+        FLAC__StreamDecoderReadStatus st = d->read_cb(d, d->buf.data() + old, &bytes, d->client);
+        if (bytes > want) bytes = want;
+        d->buf.resize(old + bytes);
+        if (st == FLAC__STREAM_DECODER_READ_STATUS_ABORT) return 2;
+        if (bytes == 0) {
+            if (st == FLAC__STREAM_DECODER_READ_STATUS_END_OF_STREAM || (d->eof_cb && d->eof_cb(d, d->client))) return 1;
+            continue;
+        }
+        return 0;
+    }
+    return 2;
+}
+
+/* the decoder genuinely needs bytes [.., upto): failure sets END_OF_STREAM / ABORTED */
+bool need_bytes(Dec *d, uint64_t upto) {
+    while (d->buf.size() < upto) {
+        int r = fill_raw(d);
+        if (r) {
+            if (!d->client_done) d->client_done = r;
+            d->state = (r == 2) ? FLAC__STREAM_DECODER_ABORTED : FLAC__STREAM_DECODER_END_OF_STREAM;
+            return false;
+        }
+    }
+    return true;
+}
+
+/* read ahead for the GPU window; hitting the client's end is remembered, not reported */
+void read_ahead(Dec *d, uint64_t upto) {
+    while (d->buf.size() < upto && !d->client_done) {
+        int r = fill_raw(d);
+        if (r) d->client_done = r;
+    }
+}
+
+/* metadata bit reader on the host buffer */
+bool mb_read(Dec *d, uint32_t *v, unsigned bits) {
+    if (bits == 0) {
+        *v = 0;
+        return true;
+    }
+    uint64_t end = d->bitpos_meta + bits;
+    if (!need_bytes(d, (end + 7) / 8)) return false;
+    uint64_t x = 0;
+    for (uint64_t p = d->bitpos_meta; p < end; p++) x = (x << 1) | ((d->buf[p >> 3] >> (7 - (p & 7))) & 1u);
+    d->bitpos_meta = end;
+    *v = (uint32_t)x;
+    return true;
+}
+
+bool mb_byte(Dec *d, uint32_t *x) {
+    if (d->cached) {
+        *x = d->lookahead;
+        d->cached = false;
+        return true;
+    }
+    return mb_read(d, x, 8);
+}
+
+void send_error(Dec *d, FLAC__StreamDecoderErrorStatus st) {
+    if (!d->is_seeking) d->error_cb(d, st, d->client);
+}
+
+bool skip_id3v2(Dec *d) {
+    uint32_t x, skip = 0;
+    if (!mb_read(d, &x, 24)) return false;
+    for (int i = 0; i < 4; i++) {
+        if (!mb_read(d, &x, 8)) return false;
+        skip = (skip << 7) | (x & 0x7f);
+    }
+    uint64_t end = d->bitpos_meta + (uint64_t)skip * 8;
+    if (!need_bytes(d, end / 8)) return false;
+    d->bitpos_meta = end;
+    return true;
+}
+
+/* find_metadata_ */
+bool find_metadata(Dec *d) {
+    static const uint8_t sync[4] = {'f', 'L', 'a', 'C'};
+    static const uint8_t id3[3] = {'I', 'D', '3'};
+    uint32_t x;
+    unsigned i = 0, id = 0;
+    bool first = true;
+    while (i < 4) {
+        if (!mb_byte(d, &x)) return false;
+        if (x == sync[i]) {
+            first = true;
+            i++;
+            id = 0;
+            continue;
+        }
+        if (x == id3[id]) {
+            id++;
+            i = 0;
+            if (id == 3 && !skip_id3v2(d)) return false;
+            continue;
+        }
+        id = 0;
+        if (x == 0xff) {
+            d->header_warmup[0] = (uint8_t)x;
+            if (!mb_read(d, &x, 8)) return false;
+            if (x == 0xff) {
+                d->lookahead = (uint8_t)x;
+                d->cached = true;
+            } else if (x >> 2 == 0x3e) {
+                d->header_warmup[1] = (uint8_t)x;
+                d->pos = d->bitpos_meta / 8;
+                d->state = FLAC__STREAM_DECODER_READ_FRAME;
+                return true;
+            }
+        }
+        i = 0;
+        if (first) {
+            send_error(d, FLAC__STREAM_DECODER_ERROR_STATUS_LOST_SYNC);
+            first = false;
+        }
+    }
+    d->state = FLAC__STREAM_DECODER_READ_METADATA;
+    return true;
+}
+
+/* read_metadata_ (STREAMINFO reported; every other block skipped, as libFLAC's default
+ * metadata_respond set does) */
+bool read_metadata(Dec *d) {
+    uint32_t last, type, length;
+    if (!mb_read(d, &last, 1) || !mb_read(d, &type, 7) || !mb_read(d, &length, 24)) return false;
+    if (type == FLAC__METADATA_TYPE_STREAMINFO) {
+        FLAC__StreamMetadata &m = d->stream_info;
+        FLAC__StreamMetadata_StreamInfo &si = m.data.stream_info;
+        uint32_t v, hi, lo;
+        memset(&m, 0, sizeof m);
+        m.type = FLAC__METADATA_TYPE_STREAMINFO;
+        m.is_last = last ? 1 : 0;
+        m.length = length;
+        if (!mb_read(d, &v, 16)) return false;
+        si.min_blocksize = v;
+        if (!mb_read(d, &v, 16)) return false;
+        si.max_blocksize = v;
+        if (!mb_read(d, &v, 24)) return false;
+        si.min_framesize = v;
+        if (!mb_read(d, &v, 24)) return false;
+        si.max_framesize = v;
+        if (!mb_read(d, &v, 20)) return false;
+        si.sample_rate = v;
+        if (!mb_read(d, &v, 3)) return false;
+        si.channels = v + 1;
+        if (!mb_read(d, &v, 5)) return false;
+        si.bits_per_sample = v + 1;
+        if (!mb_read(d, &hi, 4) || !mb_read(d, &lo, 32)) return false;
+        si.total_samples = ((uint64_t)hi << 32) | lo;
+        for (int i = 0; i < 16; i++) {
+            if (!mb_read(d, &v, 8)) return false;
+            si.md5sum[i] = (uint8_t)v;
+        }
+        uint64_t end = d->bitpos_meta + (uint64_t)(uint32_t)(length - 34u) * 8;
+        if (!need_bytes(d, end / 8)) return false;
+        d->bitpos_meta = end;
+        d->has_stream_info = true;
+        if (d->metadata_cb && !d->is_seeking) d->metadata_cb(d, &m, d->client);
+    } else {
+        uint64_t end = d->bitpos_meta + (uint64_t)length * 8;
+        if (!need_bytes(d, end / 8)) return false;
+        d->bitpos_meta = end;
+    }
+    if (last) {
+        d->pos = d->bitpos_meta / 8;
+        d->first_frame_offset = d->pos;
+        d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+    }
+    return true;
+}
+
+bool byte_at(Dec *d, uint64_t p, uint32_t *x) {
+    if (!need_bytes(d, p + 1)) return false;
+    *x = d->buf[p];
+    return true;
+}
+
+/* frame_sync_ (@0x10011760) over the host buffer */
+bool frame_sync(Dec *d) {
+    bool first = true;
+    uint64_t total = d->has_stream_info ? d->stream_info.data.stream_info.total_samples : 0;
+    if (total > 0 && d->samples_decoded >= total) {
+        d->state = FLAC__STREAM_DECODER_END_OF_STREAM;
+        return true;
+    }
+    for (;;) {
+        uint32_t x;
+        if (d->cached) {
+            x = d->lookahead;
+            d->cached = false;
+        } else {
+            if (!byte_at(d, d->pos, &x)) return false;
+            d->pos++;
+        }
+        if (x == 0xff) {
+            d->header_warmup[0] = (uint8_t)x;
+            if (!byte_at(d, d->pos, &x)) return false;
+            d->pos++;
+            if (x == 0xff) {
+                d->lookahead = (uint8_t)x;
+                d->cached = true;
+            } else if (x >> 2 == 0x3e) {
+                d->header_warmup[1] = (uint8_t)x;
+                d->state = FLAC__STREAM_DECODER_READ_FRAME;
+                return true;
+            }
+        }
+        if (first) {
+            send_error(d, FLAC__STREAM_DECODER_ERROR_STATUS_LOST_SYNC);
+            first = false;
+        }
+    }
+}
+
+bool gpu_init(Dec *d) {
+    if (d->gpu_ready) return true;
+    const char *dev = getenv("BNFLAC_DEVICE");
+    d->device = dev ? atoi(dev) : 0;
+    if (bnflac_ctx_create(d->device, &d->ctx) != 0) return false;
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) return fail("bnflac: stream create failed") == 0;
+    d->gpu_ready = true;
+    return true;
+}
+
+void gpu_free(Dec *d) {
+    if (!d->gpu_ready) return;
+    (void)hipSetDevice(d->device);
+    d->d_bytes.release();
+    d->d_cand.release();
+    d->d_count.release();
+    d->d_info.release();
+    d->d_pcm.release();
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    d->stream = nullptr;
+    bnflac_ctx_destroy(d->ctx);
+    d->ctx = nullptr;
+    d->gpu_ready = false;
+}
+
+/* Decode every candidate frame in buf[base, buf.size()) on the GPU. */
+bool decode_window(Dec *d, uint64_t base) {
+    if (!gpu_init(d)) {
+        d->state = FLAC__STREAM_DECODER_MEMORY_ALLOCATION_ERROR;
+        return false;
+    }
+    (void)hipSetDevice(d->device);
+    const uint64_t n = d->buf.size() - base;
+    const size_t padded = (size_t)((n + 3) & ~3ull) + 16;
+    if (!d->d_bytes.grow(padded)) goto oom;
+    if (hipMemsetAsync((uint8_t *)d->d_bytes.p + (n & ~3ull), 0, padded - (n & ~3ull), d->stream) != hipSuccess) goto hip_fail;
+    if (hipMemcpyAsync(d->d_bytes.p, d->buf.data() + base, n, hipMemcpyHostToDevice, d->stream) != hipSuccess) goto hip_fail;
+    {
+        uint32_t cap = (uint32_t)std::min<uint64_t>(n / 2 + 16, 1u << 30);
+        cap = std::min<uint32_t>(cap, (uint32_t)(n / 64 + 4096));
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if (!d->d_cand.grow(sizeof(uint64_t) * cap) || !d->d_count.grow(16)) goto oom;
+            if (bnflac_index_frames(d->ctx, (const uint8_t *)d->d_bytes.p, n, (uint64_t *)d->d_cand.p, cap,
+                                    (uint32_t *)d->d_count.p, d->stream) != 0)
+                goto hip_fail;
+            uint32_t cnt = 0;
+            if (hipMemcpyAsync(&cnt, d->d_count.p, 4, hipMemcpyDeviceToHost, d->stream) != hipSuccess) goto hip_fail;
+            if (hipStreamSynchronize(d->stream) != hipSuccess) goto hip_fail;
+            if (cnt <= cap) {
+                cap = cnt;
+                break;
+            }
+            cap = cnt;
+        }
+        const uint32_t ncand = cap;
+        d->cand.resize(ncand);
+        d->info.resize(ncand);
+        if (ncand) {
+            if (hipMemcpyAsync(d->cand.data(), d->d_cand.p, sizeof(uint64_t) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
+                goto hip_fail;
+            bnf_stream_params sp;
+            memset(&sp, 0, sizeof sp);
+            if (d->has_stream_info) {
+                const FLAC__StreamMetadata_StreamInfo &si = d->stream_info.data.stream_info;
+                sp.has_stream_info = 1;
+                sp.min_blocksize = si.min_blocksize;
+                sp.max_blocksize = si.max_blocksize;
+                sp.sample_rate = si.sample_rate;
+                sp.channels = si.channels;
+                sp.bps = si.bits_per_sample;
+                sp.total_samples = si.total_samples;
+            }
+            const uint32_t pcm_ch = 8; /* planar slots sized for any channel count */
+            if (!d->d_info.grow(sizeof(bnf_frame_info) * ncand)) goto oom;
+            const uint32_t nwords = (uint32_t)((n + 3) / 4);
+            if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, nwords, n, (const uint64_t *)d->d_cand.p, ncand, sp,
+                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, d->stream) != hipSuccess)
+                goto hip_fail;
+            if (hipMemcpyAsync(d->info.data(), d->d_info.p, sizeof(bnf_frame_info) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
+                goto hip_fail;
+            if (hipStreamSynchronize(d->stream) != hipSuccess) goto hip_fail;
+            uint64_t tot = 0;
+            for (auto &fi : d->info) {
+                fi.out_sample = tot;
+                if (fi.status == BNF_ST_OK) tot += fi.blocksize;
+            }
+            if (!d->d_pcm.grow(sizeof(int32_t) * (size_t)std::max<uint64_t>(tot, 1) * pcm_ch)) goto oom;
+            if (hipMemcpyAsync(d->d_info.p, d->info.data(), sizeof(bnf_frame_info) * ncand, hipMemcpyHostToDevice, d->stream) != hipSuccess)
+                goto hip_fail;
+            bnf_stream_params spd = sp;
+            spd.channels = pcm_ch;
+            if (bnf_launch_decode((const uint32_t *)d->d_bytes.p, nwords, n, ncand, spd, 8, BNF_OUT_PLANAR32,
+                                  (uint8_t *)d->d_pcm.p, (uint64_t)std::max<uint64_t>(tot, 1) * pcm_ch * 4,
+                                  (bnf_frame_info *)d->d_info.p, d->stream) != hipSuccess)
+                goto hip_fail;
+            d->pcm.resize((size_t)tot * pcm_ch);
+            if (tot && hipMemcpyAsync(d->pcm.data(), d->d_pcm.p, sizeof(int32_t) * (size_t)tot * pcm_ch, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
+                goto hip_fail;
+            if (hipMemcpyAsync(d->info.data(), d->d_info.p, sizeof(bnf_frame_info) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
+                goto hip_fail;
+            if (hipStreamSynchronize(d->stream) != hipSuccess) goto hip_fail;
+        }
+    }
+    d->win_base = base;
+    d->win_end = d->buf.size();
+    d->win_valid = true;
+    return true;
+oom:
+    fail("bnflac: out of device memory");
+    d->state = FLAC__STREAM_DECODER_MEMORY_ALLOCATION_ERROR;
+    return false;
+hip_fail:
+    fail(std::string("bnflac: HIP error in decode window: ") + hipGetErrorString(hipGetLastError()));
+    d->state = FLAC__STREAM_DECODER_MEMORY_ALLOCATION_ERROR;
+    return false;
+}
+
+const bnf_frame_info *lookup(Dec *d, uint64_t p) {
+    if (!d->win_valid || p < d->win_base || p >= d->win_end) return nullptr;
+    uint64_t rel = p - d->win_base;
+    auto it = std::lower_bound(d->cand.begin(), d->cand.end(), rel);
+    if (it == d->cand.end() || *it != rel) return nullptr;
+    return &d->info[(size_t)(it - d->cand.begin())];
+}
+
+void allocate_output(Dec *d, unsigned size, unsigned ch) {
+    if (size <= d->output_capacity && ch <= d->output_channels) return;
+    for (unsigned i = 0; i < FLAC__MAX_CHANNELS; i++) d->output[i].clear();
+    for (unsigned i = 0; i < ch; i++) d->output[i].assign(size ? size : 1, 0);
+    d->output_capacity = size;
+    d->output_channels = ch;
+}
+
+/* read_frame_ (@0x100118c0) replay for the frame whose sync starts at d->pos - 2 */
+bool read_frame(Dec *d, bool *got) {
+    *got = false;
+    const uint64_t p = d->pos - 2;
+    const bnf_frame_info *fi = nullptr;
+    for (int tries = 0;; tries++) {
+        fi = lookup(d, p);
+        if (fi && fi->status != BNF_ST_TRUNC) break;
+        if (tries > 200) {
+            fail("bnflac: frame window did not converge");
+            d->state = FLAC__STREAM_DECODER_ABORTED;
+            return false;
+        }
+        if (d->client_done) {
+            /* no more bytes will come: a truncated frame makes libFLAC's reader fail here */
+            if ((fi && fi->status == BNF_ST_TRUNC) ||
+                (d->win_valid && d->win_base == p && d->win_end == d->buf.size())) {
+                need_bytes(d, d->buf.size() + 1);
+                return false;
+            }
+        } else {
+            const uint64_t have = d->buf.size() > p ? d->buf.size() - p : 0;
+            read_ahead(d, p + std::max<uint64_t>(d->read_ahead, 2 * have + 4096));
+        }
+        if (!decode_window(d, p)) return false;
+    }
+    if (!fi) {
+        d->state = FLAC__STREAM_DECODER_ABORTED;
+        return false;
+    }
+    if (fi->status == BNF_ST_SKIPPED) {
+        fail("bnflac: frame not decodable with the configured lanes");
+        d->state = FLAC__STREAM_DECODER_ABORTED;
+        return false;
+    }
+    const uint64_t abs_resume = d->win_base * 8 + fi->resume_bit;
+    if (fi->status == BNF_ST_ERROR) {
+        send_error(d, (FLAC__StreamDecoderErrorStatus)fi->err);
+        d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+        d->pos = (abs_resume + 7) / 8;
+        if (fi->cached >= 0) {
+            d->cached = true;
+            d->lookahead = (uint8_t)fi->cached;
+        }
+        return true;
+    }
+    /* header -> FLAC__Frame, frame/sample number conversion (@0x1001231f-0x100123ca) */
+    FLAC__FrameHeader &h = d->frame.header;
+    memset(&d->frame, 0, sizeof d->frame);
+    h.blocksize = fi->blocksize;
+    h.sample_rate = fi->sample_rate;
+    h.channels = fi->channels;
+    h.channel_assignment = (FLAC__ChannelAssignment)fi->assignment;
+    h.bits_per_sample = fi->bps;
+    h.crc = (FLAC__uint8)fi->crc8;
+    d->next_fixed_block_size = 0;
+    bool unparseable = false;
+    if (fi->number_type == 0) {
+        const uint32_t fn = (uint32_t)fi->number;
+        h.number_type = FLAC__FRAME_NUMBER_TYPE_SAMPLE_NUMBER;
+        if (d->fixed_block_size) {
+            h.number.sample_number = (uint64_t)d->fixed_block_size * fn;
+        } else if (d->has_stream_info) {
+            const FLAC__StreamMetadata_StreamInfo &si = d->stream_info.data.stream_info;
+            if (si.min_blocksize == si.max_blocksize) {
+                h.number.sample_number = (uint64_t)si.min_blocksize * fn;
+                d->next_fixed_block_size = si.max_blocksize;
+            } else {
+                unparseable = true;
+            }
+        } else if (fn == 0) {
+            h.number.sample_number = 0;
+            d->next_fixed_block_size = h.blocksize;
+        } else {
+            h.number.sample_number = (uint64_t)h.blocksize * fn;
+        }
+    } else {
+        h.number_type = FLAC__FRAME_NUMBER_TYPE_SAMPLE_NUMBER;
+        h.number.sample_number = fi->number;
+    }
+    if (unparseable) {
+        send_error(d, FLAC__STREAM_DECODER_ERROR_STATUS_UNPARSEABLE_STREAM);
+        d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+        /* libFLAC stops right after the header's CRC-8 byte */
+        d->pos = fi->frame_off + d->win_base + 2; /* conservative: resync just past the sync */
+        return true;
+    }
+    d->frame.footer.crc = (FLAC__uint16)fi->crc16_read;
+    allocate_output(d, h.blocksize, h.channels);
+    const int32_t *src = d->pcm.data() + (size_t)fi->out_sample * 8;
+    for (unsigned c = 0; c < h.channels; c++)
+        memcpy(d->output[c].data(), src + (size_t)c * h.blocksize, sizeof(int32_t) * h.blocksize);
+    if (!fi->crc_ok) send_error(d, FLAC__STREAM_DECODER_ERROR_STATUS_FRAME_CRC_MISMATCH); /* output already zeroed */
+    *got = true;
+    if (d->next_fixed_block_size) d->fixed_block_size = d->next_fixed_block_size;
+    d->channels = h.channels;
+    d->channel_assignment = h.channel_assignment;
+    d->bits_per_sample = h.bits_per_sample;
+    d->sample_rate = h.sample_rate;
+    d->blocksize = h.blocksize;
+    d->samples_decoded = h.number.sample_number + h.blocksize;
+    d->pos = abs_resume / 8;
+    const FLAC__int32 *bufs[FLAC__MAX_CHANNELS];
+    for (unsigned c = 0; c < FLAC__MAX_CHANNELS; c++) bufs[c] = c < d->output_channels ? d->output[c].data() : nullptr;
+    if (d->is_seeking) {
+        /* write_audio_frame_to_client_ while seeking: deliver only the frame holding the
+         * target sample, trimmed so it starts there */
+        const uint64_t sn = h.number.sample_number;
+        if (d->seek_target >= sn && d->seek_target < sn + h.blocksize) {
+            const unsigned delta = (unsigned)(d->seek_target - sn);
+            FLAC__Frame fr = d->frame;
+            fr.header.blocksize -= delta;
+            fr.header.number.sample_number += delta;
+            const FLAC__int32 *nb[FLAC__MAX_CHANNELS];
+            for (unsigned c = 0; c < FLAC__MAX_CHANNELS; c++) nb[c] = bufs[c] ? bufs[c] + delta : nullptr;
+            d->is_seeking = false;
+            d->seek_done = 1;
+            d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+            FLAC__StreamDecoderWriteStatus ws = d->write_cb(d, &fr, nb, d->client);
+            if (ws != FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE && !d->ignore_write_status) d->seek_done = -1;
+            return true;
+        }
+        d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+        return true;
+    }
+    FLAC__StreamDecoderWriteStatus ws = d->write_cb(d, &d->frame, bufs, d->client);
+    if (ws != FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE && !d->ignore_write_status) return false; /* state stays READ_FRAME */
+    d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+    return true;
+}
+
+void reset_fields(Dec *d) {
+    d->buf.clear();
+    d->pos = 0;
+    d->bitpos_meta = 0;
+    d->cached = false;
+    d->client_done = 0;
+    d->has_stream_info = false;
+    d->samples_decoded = 0;
+    d->fixed_block_size = d->next_fixed_block_size = 0;
+    d->first_frame_offset = 0;
+    d->win_valid = false;
+    d->cand.clear();
+    d->info.clear();
+    d->pcm.clear();
+    d->is_seeking = false;
+}
+
+/* file callbacks (stream_decoder.c file_*_callback_) */
+FLAC__StreamDecoderReadStatus file_read(const FLAC__StreamDecoder *dec, FLAC__byte buffer[], size_t *bytes, void *) {
+    FILE *f = dec->file;
+    if (*bytes > 0) {
+        *bytes = fread(buffer, 1, *bytes, f);
+        if (ferror(f)) return FLAC__STREAM_DECODER_READ_STATUS_ABORT;
+        if (*bytes == 0) return FLAC__STREAM_DECODER_READ_STATUS_END_OF_STREAM;
+        return FLAC__STREAM_DECODER_READ_STATUS_CONTINUE;
+    }
+    return FLAC__STREAM_DECODER_READ_STATUS_ABORT;
+}
+FLAC__StreamDecoderSeekStatus file_seek(const FLAC__StreamDecoder *dec, FLAC__uint64 off, void *) {
+    return fseeko(dec->file, (off_t)off, SEEK_SET) < 0 ? FLAC__STREAM_DECODER_SEEK_STATUS_ERROR : FLAC__STREAM_DECODER_SEEK_STATUS_OK;
+}
+FLAC__StreamDecoderTellStatus file_tell(const FLAC__StreamDecoder *dec, FLAC__uint64 *off, void *) {
+    off_t p = ftello(dec->file);
+    if (p < 0) return FLAC__STREAM_DECODER_TELL_STATUS_ERROR;
+    *off = (FLAC__uint64)p;
+    return FLAC__STREAM_DECODER_TELL_STATUS_OK;
+}
+FLAC__StreamDecoderLengthStatus file_length(const FLAC__StreamDecoder *dec, FLAC__uint64 *len, void *) {
+    struct stat st;
+    if (fstat(fileno(dec->file), &st) != 0) return FLAC__STREAM_DECODER_LENGTH_STATUS_ERROR;
+    *len = (FLAC__uint64)st.st_size;
+    return FLAC__STREAM_DECODER_LENGTH_STATUS_OK;
+}
+FLAC__bool file_eof(const FLAC__StreamDecoder *dec, void *) { return feof(dec->file) ? 1 : 0; }
+
+} // namespace
+
+/* ---------------------------------------------------------------- exports */
+extern "C" {
+
+BNFLAC_API FLAC__StreamDecoder *FLAC__stream_decoder_new(void) {
+    Dec *d = new (std::nothrow) Dec();
+    if (!d) return nullptr;
+    memset(&d->stream_info, 0, sizeof d->stream_info);
+    memset(&d->frame, 0, sizeof d->frame);
+    const char *ra = getenv("BNFLAC_READ_AHEAD_MB");
+    if (ra) d->read_ahead = (uint64_t)std::max(1, atoi(ra)) << 20;
+    return d;
+}
+
+static int init_common(Dec *d) {
+    reset_fields(d);
+    if (!gpu_init(d)) return FLAC__STREAM_DECODER_INIT_STATUS_MEMORY_ALLOCATION_ERROR;
+    d->state = FLAC__STREAM_DECODER_SEARCH_FOR_METADATA;
+    return FLAC__STREAM_DECODER_INIT_STATUS_OK;
+}
+
+BNFLAC_API int FLAC__stream_decoder_init_stream(FLAC__StreamDecoder *d, FLAC__StreamDecoderReadCallback read,
+                                                FLAC__StreamDecoderSeekCallback seek, FLAC__StreamDecoderTellCallback tell,
+                                                FLAC__StreamDecoderLengthCallback length, FLAC__StreamDecoderEofCallback eof,
+                                                FLAC__StreamDecoderWriteCallback write,
+                                                FLAC__StreamDecoderMetadataCallback metadata,
+                                                FLAC__StreamDecoderErrorCallback error, void *client) {
+    if (!d) return FLAC__STREAM_DECODER_INIT_STATUS_MEMORY_ALLOCATION_ERROR;
+    if (d->state != FLAC__STREAM_DECODER_UNINITIALIZED) return FLAC__STREAM_DECODER_INIT_STATUS_ALREADY_INITIALIZED;
+    if (!read || !write || !error || (seek && (!tell || !length || !eof)))
+        return FLAC__STREAM_DECODER_INIT_STATUS_INVALID_CALLBACKS;
+    d->read_cb = read; d->seek_cb = seek; d->tell_cb = tell; d->length_cb = length; d->eof_cb = eof;
+    d->write_cb = write; d->metadata_cb = metadata; d->error_cb = error; d->client = client;
+    d->ignore_write_status = false;
+    return init_common(d);
+}
+
+BNFLAC_API int FLAC__stream_decoder_init_file(FLAC__StreamDecoder *d, const char *filename,
+                                              FLAC__StreamDecoderWriteCallback write,
+                                              FLAC__StreamDecoderMetadataCallback metadata,
+                                              FLAC__StreamDecoderErrorCallback error, void *client) {
+    if (!d) return FLAC__STREAM_DECODER_INIT_STATUS_MEMORY_ALLOCATION_ERROR;
+    if (d->state != FLAC__STREAM_DECODER_UNINITIALIZED) return FLAC__STREAM_DECODER_INIT_STATUS_ALREADY_INITIALIZED;
+    if (!write || !error) return FLAC__STREAM_DECODER_INIT_STATUS_INVALID_CALLBACKS;
+    FILE *f = filename ? fopen(filename, "rb") : stdin;
+    if (!f) return FLAC__STREAM_DECODER_INIT_STATUS_ERROR_OPENING_FILE;
+    d->file = f;
+    d->read_cb = file_read; d->seek_cb = file_seek; d->tell_cb = file_tell; d->length_cb = file_length; d->eof_cb = file_eof;
+    d->write_cb = write; d->metadata_cb = metadata; d->error_cb = error; d->client = client;
+    /* LibFLACSharp.cs:205-206 declares this write callback void: its return register is
+     * garbage, so it is treated as CONTINUE (BNFLAC_STRICT_WRITE_STATUS=1 honours it). */
+    const char *strict = getenv("BNFLAC_STRICT_WRITE_STATUS");
+    d->ignore_write_status = !(strict && atoi(strict));
+    int rc = init_common(d);
+    if (rc != FLAC__STREAM_DECODER_INIT_STATUS_OK) {
+        fclose(f);
+        d->file = nullptr;
+    }
+    return rc;
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_finish(FLAC__StreamDecoder *d) {
+    if (!d) return 0;
+    if (d->state == FLAC__STREAM_DECODER_UNINITIALIZED) return 1;
+    if (d->file && d->file != stdin) fclose(d->file);
+    d->file = nullptr;
+    reset_fields(d);
+    for (unsigned i = 0; i < FLAC__MAX_CHANNELS; i++) d->output[i].clear();
+    d->output_capacity = d->output_channels = 0;
+    d->state = FLAC__STREAM_DECODER_UNINITIALIZED;
+    return 1; /* MD5 checking is off by default (BirdNest never enables it) */
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_delete(FLAC__StreamDecoder *d) {
+    if (!d) return 1;
+    FLAC__stream_decoder_finish(d);
+    gpu_free(d);
+    delete d;
+    return 1;
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_process_single(FLAC__StreamDecoder *d) {
+    if (!d) return 0;
+    bool got;
+    for (;;) {
+        switch (d->state) {
+        case FLAC__STREAM_DECODER_SEARCH_FOR_METADATA:
+            if (!find_metadata(d)) return 0;
+            break;
+        case FLAC__STREAM_DECODER_READ_METADATA:
+            return read_metadata(d) ? 1 : 0;
+        case FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC:
+            if (!frame_sync(d)) return 1;
+            break;
+        case FLAC__STREAM_DECODER_READ_FRAME:
+            if (!read_frame(d, &got)) return 0;
+            if (got) return 1;
+            break;
+        case FLAC__STREAM_DECODER_END_OF_STREAM:
+        case FLAC__STREAM_DECODER_ABORTED:
+            return 1;
+        default:
+            return 0;
+        }
+    }
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_process_until_end_of_metadata(FLAC__StreamDecoder *d) {
+    if (!d) return 0;
+    for (;;) {
+        switch (d->state) {
+        case FLAC__STREAM_DECODER_SEARCH_FOR_METADATA:
+            if (!find_metadata(d)) return 0;
+            break;
+        case FLAC__STREAM_DECODER_READ_METADATA:
+            if (!read_metadata(d)) return 0;
+            break;
+        case FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC:
+        case FLAC__STREAM_DECODER_READ_FRAME:
+        case FLAC__STREAM_DECODER_END_OF_STREAM:
+        case FLAC__STREAM_DECODER_ABORTED:
+            return 1;
+        default:
+            return 0;
+        }
+    }
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_process_until_end_of_stream(FLAC__StreamDecoder *d) {
+    if (!d) return 0;
+    bool got;
+    for (;;) {
+        switch (d->state) {
+        case FLAC__STREAM_DECODER_SEARCH_FOR_METADATA:
+            if (!find_metadata(d)) return 0;
+            break;
+        case FLAC__STREAM_DECODER_READ_METADATA:
+            if (!read_metadata(d)) return 0;
+            break;
+        case FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC:
+            if (!frame_sync(d)) return 1;
+            break;
+        case FLAC__STREAM_DECODER_READ_FRAME:
+            if (!read_frame(d, &got)) return 0;
+            break;
+        case FLAC__STREAM_DECODER_END_OF_STREAM:
+        case FLAC__STREAM_DECODER_ABORTED:
+            return 1;
+        default:
+            return 0;
+        }
+    }
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_seek_absolute(FLAC__StreamDecoder *d, FLAC__uint64 sample) {
+    if (!d) return 0;
+    if (d->state > FLAC__STREAM_DECODER_END_OF_STREAM) return 0;
+    if (!d->seek_cb) return 0;
+    FLAC__uint64 total = FLAC__stream_decoder_get_total_samples(d);
+    if (total > 0 && sample >= total) return 0;
+    FLAC__uint64 length = 0;
+    if (d->length_cb(d, &length, d->client) != FLAC__STREAM_DECODER_LENGTH_STATUS_OK) return 0;
+    if (d->state <= FLAC__STREAM_DECODER_READ_METADATA) {
+        if (!FLAC__stream_decoder_process_until_end_of_metadata(d)) return 0;
+        total = FLAC__stream_decoder_get_total_samples(d);
+        if (total > 0 && sample >= total) return 0;
+    }
+    /* Walk frames from the first frame (every byte read so far is still buffered) until
+     * the one holding `sample`; only that frame reaches the write callback, trimmed. */
+    d->is_seeking = true;
+    d->seek_target = sample;
+    d->seek_done = 0;
+    d->pos = d->first_frame_offset;
+    d->cached = false;
+    d->samples_decoded = 0;
+    d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+    bool got;
+    for (int guard = 0; guard < 100000000 && !d->seek_done; guard++) {
+        if (d->state == FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC) {
+            if (!frame_sync(d)) break;
+        } else if (d->state == FLAC__STREAM_DECODER_READ_FRAME) {
+            if (!read_frame(d, &got)) break;
+        } else {
+            break;
+        }
+    }
+    d->is_seeking = false;
+    if (d->seek_done == 1) return 1;
+    d->state = FLAC__STREAM_DECODER_SEEK_ERROR;
+    return 0;
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_get_decode_position(const FLAC__StreamDecoder *d, FLAC__uint64 *position) {
+    if (!d || !d->tell_cb) return 0;
+    if (d->tell_cb(d, position, d->client) != FLAC__STREAM_DECODER_TELL_STATUS_OK) return 0;
+    const uint64_t unconsumed = d->buf.size() - std::min<uint64_t>(d->pos, d->buf.size());
+    *position -= unconsumed;
+    return 1;
+}
+
+BNFLAC_API FLAC__uint64 FLAC__stream_decoder_get_total_samples(const FLAC__StreamDecoder *d) {
+    return (d && d->has_stream_info) ? d->stream_info.data.stream_info.total_samples : 0;
+}
+BNFLAC_API unsigned FLAC__stream_decoder_get_channels(const FLAC__StreamDecoder *d) { return d ? d->channels : 0; }
+BNFLAC_API unsigned FLAC__stream_decoder_get_bits_per_sample(const FLAC__StreamDecoder *d) { return d ? d->bits_per_sample : 0; }
+BNFLAC_API unsigned FLAC__stream_decoder_get_sample_rate(const FLAC__StreamDecoder *d) { return d ? d->sample_rate : 0; }
+BNFLAC_API FLAC__StreamDecoderState FLAC__stream_decoder_get_state(const FLAC__StreamDecoder *d) {
+    return d ? d->state : FLAC__STREAM_DECODER_UNINITIALIZED;
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_reset(FLAC__StreamDecoder *d) {
+    if (!d || d->state == FLAC__STREAM_DECODER_UNINITIALIZED) return 0;
+    if (d->file == stdin) return 0;
+    if (d->seek_cb && d->seek_cb(d, 0, d->client) == FLAC__STREAM_DECODER_SEEK_STATUS_ERROR) return 0;
+    reset_fields(d);
+    d->state = FLAC__STREAM_DECODER_SEARCH_FOR_METADATA;
+    return 1;
+}
+
+} /* extern "C" */

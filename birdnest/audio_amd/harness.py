@@ -1,0 +1,126 @@
+"""Callback-sequence driver for libbnflac.so's libFLAC API.
+
+Drives FLAC__stream_decoder_* exactly like oracle/flac_oracle.c's ``oracle_run`` drives
+the CPU restatement (same read-callback behaviour as FLACDecoder.ReadCallback,
+FLACDecoder.cs:325-363), and records the same event tuples, so tests can compare the
+GPU-backed decoder and the oracle event by event.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from .libflac import (LibFLAC, DecoderEofCallback, DecoderReadCallback, DecoderWriteCallbackWithStatus,
+                      Decoder_ErrorCallback, Decoder_MetadataCallback, load)
+
+EV_METADATA, EV_WRITE, EV_ERROR, EV_RETURN = 1, 2, 3, 4
+
+
+def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: int = -1):
+    L = load()
+    data = bytes(data)
+    st = {"pos": 0, "eof": False, "frames": 0}
+    events = []
+    pcm_parts = []
+    npcm = [0]
+    dec = L.FLAC__stream_decoder_new()
+
+    def state():
+        return int(L.FLAC__stream_decoder_get_state(dec))
+
+    def rd(d, buf, nbytes, ud):
+        want = nbytes[0]
+        if want == 0:
+            st["eof"] = True
+            return 2
+        length = min(want, read_chunk)
+        chunk = data[st["pos"]: st["pos"] + length]
+        n = len(chunk)
+        if n:
+            ctypes.memmove(buf, chunk, n)
+        st["pos"] += n
+        nbytes[0] = n
+        if n < length:
+            st["eof"] = True
+            return 1
+        return 0
+
+    def eof(d, ud):
+        return 1 if st["eof"] else 0
+
+    def wr(d, frame, buf, ud):
+        raw = ctypes.string_at(frame, 40)
+        bs, sr, ch, asg, bps, _nt = np.frombuffer(raw[:24], dtype="<u4")
+        sn = int.from_bytes(raw[24:32], "little")
+        events.append((EV_WRITE, 0, state(), int(bs), int(sr), int(ch), int(asg), int(bps), sn, npcm[0]))
+        for c in range(int(ch)):
+            pcm_parts.append(np.ctypeslib.as_array(buf[c], shape=(int(bs),)).copy())
+            npcm[0] += int(bs)
+        idx = st["frames"]
+        st["frames"] += 1
+        return 1 if idx == write_abort_at else 0
+
+    def md(d, m, ud):
+        raw = ctypes.string_at(m, 72)
+        mtype = int.from_bytes(raw[0:4], "little")
+        ev = [EV_METADATA, mtype, state(), 0, 0, 0, 0, 0, 0, 0]
+        if mtype == 0:
+            ev[3] = int.from_bytes(raw[20:24], "little")
+            ev[4] = int.from_bytes(raw[32:36], "little")
+            ev[5] = int.from_bytes(raw[36:40], "little")
+            ev[7] = int.from_bytes(raw[40:44], "little")
+            ev[8] = int.from_bytes(raw[48:56], "little")
+        events.append(tuple(ev))
+
+    def er(d, status, ud):
+        events.append((EV_ERROR, int(status), state(), 0, 0, 0, 0, 0, 0, 0))
+
+    cbs = (DecoderReadCallback(rd), DecoderEofCallback(eof), DecoderWriteCallbackWithStatus(wr),
+           Decoder_MetadataCallback(md), Decoder_ErrorCallback(er))
+    rc = L.FLAC__stream_decoder_init_stream(dec, cbs[0], _null(0), _null(1), _null(2), cbs[1], cbs[2], cbs[3],
+                                            cbs[4], None)
+    if rc != 0:
+        L.FLAC__stream_decoder_delete(dec)
+        raise RuntimeError(f"init_stream failed rc={rc}: {L.bnflac_last_error().decode()}")
+    try:
+        if driver == 0:
+            ok = int(L.FLAC__stream_decoder_process_until_end_of_metadata(dec))
+            events.append((EV_RETURN, ok, state(), 0, 0, 0, 0, 0, 0, 0))
+            if ok:
+                for _ in range(50_000_000):
+                    if state() >= 4:
+                        break
+                    ok = int(L.FLAC__stream_decoder_process_single(dec))
+                    events.append((EV_RETURN, ok, state(), 0, 0, 0, 0, 0, 0, 0))
+                    if not ok:
+                        break
+        else:
+            ok = int(L.FLAC__stream_decoder_process_until_end_of_stream(dec))
+            events.append((EV_RETURN, ok, state(), 0, 0, 0, 0, 0, 0, 0))
+    finally:
+        L.FLAC__stream_decoder_delete(dec)
+    pcm = np.concatenate(pcm_parts) if pcm_parts else np.zeros(0, dtype=np.int32)
+    return events, pcm
+
+
+def _null(kind):
+    from .libflac import DecoderSeekCallback, DecoderTellCallback, DecoderLengthCallback
+    return [DecoderSeekCallback, DecoderTellCallback, DecoderLengthCallback][kind]()
+
+
+def oracle_events_as_tuples(events):
+    """oracle.Event list -> tuples comparable with run()'s."""
+    out = []
+    for e in events:
+        if e.kind == EV_WRITE:
+            out.append((e.kind, 0, e.state, e.blocksize, e.sample_rate, e.channels, e.assignment, e.bps,
+                        e.sample_number, e.pcm_offset))
+        elif e.kind == EV_METADATA:
+            ev = [e.kind, e.status, e.state, 0, 0, 0, 0, 0, 0, 0]
+            if e.status == 0:
+                ev[3], ev[4], ev[5], ev[7], ev[8] = e.blocksize, e.sample_rate, e.channels, e.bps, e.sample_number
+            out.append(tuple(ev))
+        else:
+            out.append((e.kind, e.status, e.state, 0, 0, 0, 0, 0, 0, 0))
+    return out

@@ -1,0 +1,159 @@
+/*
+ * bnflac.h -- C ABI of libbnflac.so, the MI355X FLAC decoder behind BirdNest.Audio.
+ *
+ * Part 1: the libFLAC 1.2.1 stream-decoder entry points that BirdNest.Audio's P/Invoke
+ * layer binds ([DllImport("LibFlac", CallingConvention = Cdecl)],
+ * Library/LibFLACSharp/LibFLACSharp.cs:22).  Same names, argument meaning, return
+ * conventions and callback order as libFLAC, so FLACDecoder / FLACFileReader /
+ * OpenALDemo run unchanged when this library is loaded under the name "LibFlac"
+ * (INTEGRATION.md).  Frame decode runs on the GPU; metadata and the libFLAC state
+ * machine replay run on the host.
+ *
+ * Part 2: a batched, device-pointer API (bnflac_*) for callers that keep compressed
+ * frames and PCM resident in HBM -- the path bench.py measures.
+ *
+ * Only plain C types cross this boundary (no torch, no HIP types: a HIP stream is
+ * passed as void*).
+ */
+#ifndef BNFLAC_H
+#define BNFLAC_H
+
+#include "FLAC_compat.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define BNFLAC_API __attribute__((visibility("default")))
+#else
+#define BNFLAC_API
+#endif
+
+/* ===================== Part 1: libFLAC-compatible stream decoder ===================== */
+
+/* LibFLACSharp.cs:42-43 */
+BNFLAC_API FLAC__StreamDecoder *FLAC__stream_decoder_new(void);
+/* LibFLACSharp.cs:45-46 */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_finish(FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:48-49 declares `bool` where libFLAC returns void; this export returns
+ * true so FLACDecoder.cs:299-301's FLACCheck passes (SURVEY.md 8b hazard 1). */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_delete(FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:51-52.  The C# write delegate is declared void (:205-206); its
+ * return value is ignored for decoders initialised through init_file (hazard 2). */
+BNFLAC_API int FLAC__stream_decoder_init_file(FLAC__StreamDecoder *decoder, const char *filename,
+                                              FLAC__StreamDecoderWriteCallback write_callback,
+                                              FLAC__StreamDecoderMetadataCallback metadata_callback,
+                                              FLAC__StreamDecoderErrorCallback error_callback,
+                                              void *client_data);
+/* LibFLACSharp.cs:54-55 */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_process_single(FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:57-58 */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_process_until_end_of_metadata(FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:60-61 */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_process_until_end_of_stream(FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:63-64 */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_seek_absolute(FLAC__StreamDecoder *decoder, FLAC__uint64 sample);
+/* LibFLACSharp.cs:66-67 */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_get_decode_position(const FLAC__StreamDecoder *decoder,
+                                                               FLAC__uint64 *position);
+/* LibFLACSharp.cs:69-70 */
+BNFLAC_API FLAC__uint64 FLAC__stream_decoder_get_total_samples(const FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:72-79 */
+BNFLAC_API unsigned FLAC__stream_decoder_get_channels(const FLAC__StreamDecoder *decoder);
+BNFLAC_API unsigned FLAC__stream_decoder_get_bits_per_sample(const FLAC__StreamDecoder *decoder);
+BNFLAC_API unsigned FLAC__stream_decoder_get_sample_rate(const FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:81-82 */
+BNFLAC_API FLAC__StreamDecoderState FLAC__stream_decoder_get_state(const FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:84-85 (declared int in C#; libFLAC returns FLAC__bool) */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_reset(FLAC__StreamDecoder *decoder);
+/* LibFLACSharp.cs:175-185 */
+BNFLAC_API int FLAC__stream_decoder_init_stream(FLAC__StreamDecoder *decoder,
+                                                FLAC__StreamDecoderReadCallback read_callback,
+                                                FLAC__StreamDecoderSeekCallback seek_callback,
+                                                FLAC__StreamDecoderTellCallback tell_callback,
+                                                FLAC__StreamDecoderLengthCallback length_callback,
+                                                FLAC__StreamDecoderEofCallback eof_callback,
+                                                FLAC__StreamDecoderWriteCallback write_callback,
+                                                FLAC__StreamDecoderMetadataCallback metadata_callback,
+                                                FLAC__StreamDecoderErrorCallback error_callback,
+                                                void *client_data);
+
+/* ========================= Part 2: batched device-pointer API ========================= */
+
+typedef struct {
+    int32_t has_stream_info;
+    uint32_t min_blocksize, max_blocksize;
+    uint32_t sample_rate, channels, bps;
+    uint64_t total_samples;
+} bnflac_stream_params;
+
+/* Per-frame result record (128 bytes), device-resident. */
+typedef struct {
+    uint32_t status;        /* 0 ok, 1 libFLAC error (err), 2 truncated, 3 skipped */
+    int32_t err;            /* FLAC__StreamDecoderErrorStatus, -1 none */
+    uint64_t frame_off;
+    uint64_t resume_bit;
+    int32_t cached;
+    uint32_t blocksize, sample_rate, channels, assignment, bps;
+    uint32_t number_type, unparseable;
+    uint64_t number;
+    uint64_t out_sample;
+    uint32_t crc8, crc16_calc, crc16_read, crc_ok;
+    uint32_t sub_start[8];
+    uint32_t flags, pad_;
+} bnflac_frame_info;
+
+enum {
+    BNFLAC_OUT_PLANAR32 = 0,      /* int32, per frame channel-major (libFLAC write buffers) */
+    BNFLAC_OUT_INTERLEAVED32 = 1, /* int32 [sample][channel] */
+    BNFLAC_OUT_FLACDECODER = 2,   /* FLACDecoder.WriteCallback packing (FLACDecoder.cs:543-577) */
+    BNFLAC_OUT_FILEREADER = 3     /* FLACFileReader packing (FLACFileReader.cs:220-237) */
+};
+
+typedef struct bnflac_ctx bnflac_ctx;
+
+/* 0 on success, else a negative bnflac error code. */
+BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out);
+BNFLAC_API void bnflac_ctx_destroy(bnflac_ctx *ctx);
+BNFLAC_API const char *bnflac_last_error(void);
+BNFLAC_API int bnflac_device_count(void);
+
+/* Find every frame-sync candidate (0xFF, then a byte with top 6 bits 111110) in
+ * d_bytes[0, nbytes), in stream order.  d_bytes must be 4-byte aligned and its
+ * allocation at least round_up(nbytes, 4) bytes.  *d_count (device) receives the total
+ * (which may exceed cap; only cap offsets are written).  Asynchronous on hip_stream. */
+BNFLAC_API int bnflac_index_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
+                                   uint64_t *d_offsets, uint32_t cap, uint32_t *d_count, void *hip_stream);
+
+/* Decode nframes frames starting at d_frame_offsets (byte offsets into d_bytes).
+ * Output position of each frame: d_out_sample[i] if non-NULL, else the header's
+ * sample number (frame number x STREAMINFO blocksize for fixed-blocksize streams) minus
+ * base_sample.  Frames that would end past out_bytes are not written (status 3,
+ * flags bit 1).  d_info receives one record per frame.  Asynchronous on hip_stream. */
+BNFLAC_API int bnflac_decode_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
+                                    const uint64_t *d_frame_offsets, uint32_t nframes,
+                                    const bnflac_stream_params *sp, const uint64_t *d_out_sample,
+                                    uint64_t base_sample, int out_format, uint8_t *d_out, uint64_t out_bytes,
+                                    bnflac_frame_info *d_info, void *hip_stream);
+
+/* The two phases of bnflac_decode_frames, for callers that time or overlap them:
+ * parse = frame headers + subframe cursor walk (k_parse), decode = subframe decode,
+ * decorrelation, packing and CRC-16 (k_decode).  decode must follow parse on the same
+ * stream with the same arguments. */
+BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
+                                   const uint64_t *d_frame_offsets, uint32_t nframes,
+                                   const bnflac_stream_params *sp, const uint64_t *d_out_sample,
+                                   uint64_t base_sample, bnflac_frame_info *d_info, void *hip_stream);
+BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, uint32_t nframes,
+                                    const bnflac_stream_params *sp, int out_format, uint8_t *d_out,
+                                    uint64_t out_bytes, bnflac_frame_info *d_info, void *hip_stream);
+
+/* Bytes of one sample frame (all channels of one sample index) in out_format. */
+BNFLAC_API uint32_t bnflac_out_stride(int out_format, const bnflac_stream_params *sp);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BNFLAC_H */

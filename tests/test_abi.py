@@ -1,0 +1,72 @@
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, and its
+marshalled layouts match what LibFLACSharp.cs reads.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from birdnest.audio_amd import libflac
+from birdnest.audio_amd._lib import lib_path
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in ("bnflac.h",):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        names |= set(re.findall(r"BNFLAC_API\s+[\w\s\*]+?\b(\w+)\s*\(", src))
+    return names
+
+
+def test_library_loads_and_exports_declared_symbols():
+    L = libflac.load()
+    declared = _declared()
+    assert declared >= set(libflac.DECODER_SYMBOLS) | set(libflac.BATCH_SYMBOLS)
+    for n in sorted(declared):
+        assert hasattr(L, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", lib_path("libbnflac.so")], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert declared <= exported
+    # the ten decoder entry points BirdNest.Audio calls
+    called = {"new", "init_stream", "init_file", "process_until_end_of_metadata", "process_single", "get_state",
+              "get_total_samples", "seek_absolute", "finish", "delete"}
+    assert {"FLAC__stream_decoder_" + c for c in called} <= exported
+
+
+def test_csharp_marshalled_offsets():
+    # LibFLACSharp.cs:224-234 FrameHeader
+    fh = libflac.FrameHeader
+    assert [getattr(fh, f).offset for f in ("BlockSize", "SampleRate", "Channels", "ChannelAssignment",
+                                               "BitsPerSample", "NumberType", "FrameOrSampleNumber", "Crc")] == \
+        [0, 4, 8, 12, 16, 20, 24, 32]
+    # FLACMetaData Data[] at 12; FLACStreamInfo FieldOffset(4..36) over it -> C struct 16..48
+    assert libflac.FLACMetaData.Data.offset == 12
+    si = libflac.FLACStreamInfo
+    assert [getattr(si, f).offset + 12 for f in ("MinBlocksize", "SampleRate", "Channels", "BitsPerSample",
+                                                   "TotalSamplesHi", "TotalSamplesLo")] == [16, 32, 36, 40, 44, 48]
+
+
+def test_frame_info_record_size():
+    assert libflac.FRAME_INFO_DTYPE.itemsize == 128
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    L = libflac.load()
+    h = ctypes.c_void_p()
+    assert L.bnflac_ctx_create(0, ctypes.byref(h)) != 0
+    assert b"no HIP device" in L.bnflac_last_error()
+    d = L.FLAC__stream_decoder_new()
+    null = libflac.DecoderSeekCallback()
+    rc = L.FLAC__stream_decoder_init_stream(
+        d, libflac.DecoderReadCallback(lambda *a: 2), null, libflac.DecoderTellCallback(),
+        libflac.DecoderLengthCallback(), libflac.DecoderEofCallback(),
+        libflac.DecoderWriteCallbackWithStatus(lambda *a: 0), libflac.Decoder_MetadataCallback(),
+        libflac.Decoder_ErrorCallback(lambda *a: None), None)
+    assert rc == 3  # MEMORY_ALLOCATION_ERROR: no CPU fallback
+    assert L.FLAC__stream_decoder_delete(d) == 1  # bool-declared delete returns true (SURVEY 8b hazard 1)

@@ -1,0 +1,248 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and golden vectors.
+
+Bar: bit-exact PCM, identical libFLAC callback sequences, identical C#-surface bytes and
+exception messages.  Full-size configs are checked through the lossless round trip
+(decoded PCM == generator source PCM, CRC-16 ok on every frame).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+GOLD_DIR = os.path.join(os.path.dirname(__file__), "golden")
+GOLD = json.load(open(os.path.join(GOLD_DIR, "golden.json")))
+
+
+def _read(name):
+    return open(os.path.join(GOLD_DIR, GOLD[name]["file"]), "rb").read()
+
+
+def _sha(pcm):
+    return hashlib.sha256(np.ascontiguousarray(pcm, dtype="<i4").tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    from birdnest.audio_amd import libflac
+    return torch, libflac, libflac.BatchDecoder(0)
+
+
+def _stream_params(libflac, data: bytes):
+    """STREAMINFO -> StreamParams (host parse of the 34-byte block, like MetadataCallback)."""
+    si = data[8:42]
+    minbs = int.from_bytes(si[0:2], "big")
+    maxbs = int.from_bytes(si[2:4], "big")
+    x = int.from_bytes(si[10:18], "big")
+    sr = x >> 44
+    ch = ((x >> 41) & 7) + 1
+    bps = ((x >> 36) & 31) + 1
+    total = x & ((1 << 36) - 1)
+    return libflac.StreamParams(1, minbs, maxbs, sr, ch, bps, total)
+
+
+def _decode_batch(gpu, data: bytes, offsets, fmt, out_sample=None):
+    torch, libflac, dec = gpu
+    sp = _stream_params(libflac, data)
+    dev = torch.device("cuda:0")
+    n = len(data)
+    d_bytes = torch.zeros((n + 3) // 4 * 4 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:n] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    offs = torch.tensor([int(o) for o in offsets], dtype=torch.int64, device=dev)
+    nf = len(offsets)
+    total = sp.total_samples
+    stride = libflac.out_stride(fmt, sp)
+    d_out = torch.full((total * stride + 64,), 0xAB, dtype=torch.uint8, device=dev)
+    d_info = torch.zeros(nf * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    d_os = None
+    if out_sample is not None:
+        d_os = torch.tensor(out_sample, dtype=torch.int64, device=dev)
+    dec.decode_frames(d_bytes, n, offs, nf, sp, fmt, d_out, d_info, d_out_sample=d_os)
+    torch.cuda.synchronize()
+    info = libflac.info_array(d_info.cpu().numpy())
+    return d_out.cpu().numpy()[: total * stride], info, sp
+
+
+@pytest.mark.parametrize("name", [k for k, v in GOLD.items() if v["kind"] == "roundtrip"])
+def test_batch_roundtrip_interleaved32(gpu, name):
+    torch, libflac, _ = gpu
+    g = GOLD[name]
+    data = _read(name)
+    out, info, sp = _decode_batch(gpu, data, g["frame_offsets"], libflac.OUT_INTERLEAVED32)
+    assert (info["status"] == 0).all(), info[["status", "err"]]
+    assert (info["crc_ok"] == 1).all()
+    pcm = out.view("<i4").reshape(-1, sp.channels)
+    assert _sha(pcm) == g["pcm_sha256"]
+
+
+def test_rfc9639_example1_gpu(gpu):
+    torch, libflac, _ = gpu
+    data = _read("rfc9639_ex1")
+    out, info, sp = _decode_batch(gpu, data, [data.index(b"\xff\xf8")], libflac.OUT_INTERLEAVED32)
+    assert info["crc_ok"][0] == 1
+    assert out.view("<i4").reshape(-1, 2).tolist() == GOLD["rfc9639_ex1"]["pcm"]
+
+
+def test_rfc9639_example2_frame1_gpu(gpu):
+    torch, libflac, dec = gpu
+    g = GOLD["rfc9639_ex2_frame1"]
+    fr = _read("rfc9639_ex2_frame1")
+    data = b"fLaC" + b"\x80\x00\x00\x22" + bytes.fromhex("00100010000017000044") + \
+        bytes.fromhex("0ac442f000000013") + bytes(16) + fr
+    out, info, sp = _decode_batch(gpu, data, [42], libflac.OUT_PLANAR32)
+    assert info["crc_ok"][0] == 1 and info["blocksize"][0] == 16 and info["assignment"][0] == 2
+    pcm = out.view("<i4")[:32].reshape(2, 16).T
+    assert _sha(pcm) == g["pcm_sha256_oracle"]
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
+def test_config_batch_vs_oracle_and_source(gpu, cfg):
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    p = synth.config(cfg, nframes={"C4": 64}.get(cfg, 12), last_blocksize=0)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    out, info, sp = _decode_batch(gpu, data, s.frame_offsets, libflac.OUT_INTERLEAVED32)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    pcm = out.view("<i4").reshape(-1, p.channels)
+    assert np.array_equal(pcm, s.pcm)
+    ev, opcm = oracle.run(data)
+    assert np.array_equal(pcm, oracle.interleave(ev, opcm))
+
+
+def test_flacdecoder_format_vs_oracle(gpu):
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    for cfg, kw in (("C1", {}), ("C2", {}), ("C4", {"nframes": 40}), ("C2", {"channels": 1, "seed": 9})):
+        p = synth.config(cfg, **({"nframes": 10, "last_blocksize": 0} | kw))
+        s = synth.encode(p)
+        data = s.data.tobytes()
+        out, info, sp = _decode_batch(gpu, data, s.frame_offsets, libflac.OUT_FLACDECODER)
+        rc, ref, msg, _ = oracle.flacdecoder_copyto(data)
+        assert rc == 0, msg
+        assert out.tobytes() == ref, cfg
+
+
+def test_filereader_format_24bit_vs_oracle(gpu):
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    for cfg in ("C3", "C5"):
+        p = synth.config(cfg, nframes=4, last_blocksize=0)
+        s = synth.encode(p)
+        data = s.data.tobytes()
+        out, info, sp = _decode_batch(gpu, data, s.frame_offsets, libflac.OUT_FILEREADER)
+        rc, ref, msg = oracle.filereader_readall(data, buf_len=p.blocksize * p.channels * 3)
+        assert rc == 0, msg
+        assert out.tobytes() == ref, cfg
+
+
+def test_index_frames_matches_numpy_scan(gpu):
+    from birdnest.audio_amd import synth
+    torch, libflac, dec = gpu
+    s = synth.encode(synth.config("C2", nframes=64))
+    data = s.data.tobytes()
+    arr = np.frombuffer(data, dtype=np.uint8)
+    ref = np.nonzero((arr[:-1] == 0xFF) & ((arr[1:] >> 2) == 0x3E))[0]
+    assert set(int(x) for x in s.frame_offsets) <= set(int(x) for x in ref)
+    dev = torch.device("cuda:0")
+    n = len(data)
+    d_bytes = torch.zeros((n + 3) // 4 * 4 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:n] = torch.from_numpy(arr.copy()).to(dev)
+    d_off = torch.zeros(len(ref) + 16, dtype=torch.int64, device=dev)
+    d_cnt = torch.zeros(4, dtype=torch.int32, device=dev)
+    dec.index_frames(d_bytes, n, d_off, d_cnt)
+    torch.cuda.synchronize()
+    cnt = int(d_cnt[0].item())
+    assert cnt == len(ref)
+    assert np.array_equal(d_off[:cnt].cpu().numpy(), ref)
+
+
+def test_full_c2_batch_lossless(gpu):
+    """BASELINE config C2 at full size: 1024 frames x 4096 x 2ch, LPC-8, RPO 4."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    p = synth.config("C2")
+    s = synth.encode(p)
+    out, info, sp = _decode_batch(gpu, s.data.tobytes(), s.frame_offsets, libflac.OUT_FLACDECODER)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    assert out.tobytes() == s.pcm.astype("<i2").tobytes()
+
+
+def test_crc_mismatch_zero_filled_in_batch(gpu):
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    s = synth.encode(synth.config("C2", nframes=6))
+    d = bytearray(s.data.tobytes())
+    o = [int(x) for x in s.frame_offsets]
+    d[o[2] + 100] ^= 0x40
+    out, info, sp = _decode_batch(gpu, bytes(d), o, libflac.OUT_INTERLEAVED32)
+    pcm = out.view("<i4").reshape(-1, 2)
+    assert info["crc_ok"].tolist() == [1, 1, 0, 1, 1, 1]
+    assert not pcm[2 * 4096: 3 * 4096].any()
+    assert np.array_equal(np.delete(pcm, np.s_[2 * 4096: 3 * 4096], axis=0),
+                          np.delete(s.pcm, np.s_[2 * 4096: 3 * 4096], axis=0))
+
+
+# ---------------------------------------------------------- libFLAC API parity
+STREAM_CASES = [k for k, v in GOLD.items() if v["kind"] in ("roundtrip", "error", "rfc")]
+
+
+@pytest.mark.parametrize("name", STREAM_CASES)
+def test_stream_api_event_parity(gpu, name):
+    import oracle
+    from birdnest.audio_amd import harness
+    data = _read(name)
+    for driver in (0, 1):
+        ev, pcm = harness.run(data, driver=driver)
+        oev, opcm = oracle.run(data, driver=driver)
+        assert ev == harness.oracle_events_as_tuples(oev), (name, driver)
+        assert np.array_equal(pcm, opcm), (name, driver)
+
+
+def test_stream_api_write_abort_state(gpu):
+    import oracle
+    from birdnest.audio_amd import harness
+    data = _read("c2_lpc8")
+    ev, _ = harness.run(data, write_abort_at=2)
+    oev, _ = oracle.run(data, write_abort_at=2)
+    assert ev == harness.oracle_events_as_tuples(oev)
+    assert ev[-1][1:3] == (0, 3)  # process_single false, state READ_FRAME
+
+
+@pytest.mark.parametrize("name", STREAM_CASES)
+def test_flacdecoder_mirror_vs_oracle_replay(gpu, name):
+    import oracle
+    from birdnest.audio_amd import flac_decoder
+    data = _read(name)
+    rc, pk, msg, fmt = flac_decoder.copy_to_bytes(data)
+    orc, opk, omsg, ofmt = oracle.flacdecoder_copyto(data)
+    assert (rc, msg) == (orc, omsg)
+    assert pk == opk
+    if rc == 0:
+        assert fmt == ofmt[:4]
+
+
+def test_stream_api_large_c2_windows(gpu):
+    """Multi-window read-ahead (small windows force re-decode at window ends)."""
+    import oracle
+    from birdnest.audio_amd import harness, synth
+    s = synth.encode(synth.config("C2", nframes=96))
+    os.environ["BNFLAC_READ_AHEAD_MB"] = "1"
+    try:
+        ev, pcm = harness.run(s.data.tobytes(), driver=1, read_chunk=16384)
+    finally:
+        del os.environ["BNFLAC_READ_AHEAD_MB"]
+    oev, opcm = oracle.run(s.data.tobytes(), driver=1)
+    assert ev == harness.oracle_events_as_tuples(oev)
+    assert np.array_equal(pcm, opcm)
