@@ -45,6 +45,9 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
+    ap.add_argument("--ablate", default=None,
+                    help="comma list of ablation bitmasks to time after the measurement (timing only, wrong output): "
+                         "1 CRC, 2 stores, 4 restore, 8 rice, 16 parse walk")
     return ap.parse_args()
 
 
@@ -182,6 +185,20 @@ def main():
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(t_decode, 4),
                      "k_parse_avg_ms": round(t_parse, 4), "step_achieved_GBs": round(step_achieved, 1)},
     }
+    if args.ablate and rank == 0:
+        abl = []
+        for m in [int(x, 0) for x in args.ablate.split(",")]:
+            dec.L.bnflac_debug_set_ablate(m)
+            for _ in range(2):
+                step()
+            evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+            for k in range(args.steps):
+                step(evs[k])
+            torch.cuda.synchronize(dev)
+            abl.append({"ablate": m, "k_parse_ms": round(sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps, 4),
+                        "k_decode_ms": round(sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps, 4)})
+        dec.L.bnflac_debug_set_ablate(0)
+        line["ablation"] = abl
     if rank == 0 and not args.no_cpu_baseline:
         sys.stdout.flush()
         mss, passes, el = cpu_baseline(data, samples_per_batch, args.cpu_seconds)

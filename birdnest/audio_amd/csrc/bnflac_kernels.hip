@@ -22,6 +22,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "bnflac_device.h"
 
@@ -467,7 +468,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint32_t nwords, uint64_t nbytes,
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
-                                              uint64_t base_sample, bnf_frame_info *__restrict__ info) {
+                                              uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate) {
     uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
     bnf_frame_info fi;
@@ -502,6 +503,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
         for (uint32_t ch = 0; ch < fi.channels; ch++) {
             fi.sub_start[ch] = (uint32_t)(br_pos(b) - fbit);
             if (ch + 1 == fi.channels) break; /* the last subframe is walked by k_decode */
+            if (ablate & 16u) { fi.sub_start[ch + 1] = fi.sub_start[ch]; continue; }
             SubHdr h;
             int32_t err = -1;
             uint32_t bps = sub_bps(fi, ch);
@@ -753,7 +755,7 @@ DEV void pack_chunk(const int32_t *lds, uint32_t lane, uint32_t fpb, uint32_t ch
 __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict__ words, uint32_t nwords, uint64_t nbytes,
                                                       uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                       int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
-                                                      bnf_frame_info *__restrict__ info) {
+                                                      bnf_frame_info *__restrict__ info, uint32_t ablate) {
     __shared__ int32_t lds[DEC_LANES * ROW];
     __shared__ uint32_t f_bs[DEC_LANES], f_ch[DEC_LANES], f_as[DEC_LANES], f_ok[DEC_LANES];
     __shared__ uint64_t f_out[DEC_LANES];
@@ -883,9 +885,15 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
         if (nvalid) {
             if (h.type == T_FIXED || h.type == T_LPC || h.type == T_VERB) {
                 const uint32_t i0 = (n0 < h.order) ? h.order - n0 : 0u;
-                for (uint32_t i = i0; i < nvalid; i++) row[i] = next_val(b, rs, limit, trunc);
+                if (ablate & 8u) {
+                    for (uint32_t i = i0; i < nvalid; i++) row[i] = (int32_t)i;
+                } else {
+                    for (uint32_t i = i0; i < nvalid; i++) row[i] = next_val(b, rs, limit, trunc);
+                }
             }
-            if (h.type == T_CONST) {
+            if (ablate & 4u) {
+                /* restore skipped (timing ablation) */
+            } else if (h.type == T_CONST) {
                 for (uint32_t i = 0; i < nvalid; i++) row[i] = (int32_t)((uint32_t)h.cval << h.wasted);
             } else if (h.type == T_VERB) {
                 for (uint32_t i = 0; i < nvalid; i++) row[i] = (int32_t)((uint32_t)row[i] << h.wasted);
@@ -906,7 +914,9 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
             }
         }
         __syncthreads();
-        switch (fmt) {
+        switch ((ablate & 2u) ? -1 : fmt) {
+        case -1:
+            break;
         case BNF_OUT_PLANAR32:
             pack_chunk<BNF_OUT_PLANAR32>(lds, lane, fpb, chn_lanes, n0, f_bs, f_ch, f_as, f_out, f_ok, sp.channels, 0, out);
             break;
@@ -978,13 +988,16 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
         const uint32_t nl = fi.channels;
         const uint64_t per = (len + nl - 1) / nl;
         const uint64_t s0 = fi.frame_off + min(len, per * ch), s1 = fi.frame_off + min(len, per * (ch + 1));
-        part = crc16_range(words, nwords, s0, s1);
-        seg_end = s1;
-        part = crc16_shift(part, fi.frame_off + len - seg_end);
+        if (!(ablate & 1u)) {
+            part = crc16_range(words, nwords, s0, s1);
+            seg_end = s1;
+            part = crc16_shift(part, fi.frame_off + len - seg_end);
+        }
     }
     /* xor-reduce within each frame's lane group */
     uint32_t acc = part;
     for (uint32_t o = 1; o < chn_lanes; o <<= 1) acc ^= __shfl_xor(acc, o);
+    if ((ablate & 1u) && last && fi.status == BNF_ST_OK) acc = fi.crc16_read;
     if (last && fi.status == BNF_ST_OK) {
         fi.crc16_calc = acc;
         fi.crc_ok = (acc == fi.crc16_read) ? 1u : 0u;
@@ -1040,12 +1053,23 @@ uint32_t bnf_scan_blocks(uint64_t n) {
     return (uint32_t)((n + per_block - 1) / per_block);
 }
 
+static uint32_t g_ablate = 0xFFFFFFFFu;
+static uint32_t ablate_flags() {
+    if (g_ablate == 0xFFFFFFFFu) {
+        const char *e = getenv("BNFLAC_ABLATE"); /* timing experiments only: results are wrong */
+        g_ablate = e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+    }
+    return g_ablate;
+}
+
+void bnf_set_ablate(uint32_t v) { g_ablate = v; }
+
 hipError_t bnf_launch_parse(const uint32_t *words, uint32_t nwords, uint64_t nbytes, const uint64_t *frame_offs,
                             uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
                             uint64_t base_sample, bnf_frame_info *info, hipStream_t s) {
     if (!nframes) return hipSuccess;
     hipLaunchKernelGGL(k_parse, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nwords, nbytes, frame_offs, nframes,
-                       sp, out_sample_in, base_sample, info);
+                       sp, out_sample_in, base_sample, info, ablate_flags());
     return hipGetLastError();
 }
 
@@ -1055,7 +1079,7 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint32_t nwords, uint64_t nb
     if (!nframes) return hipSuccess;
     const uint32_t fpb = DEC_LANES / chn_lanes;
     hipLaunchKernelGGL(k_decode, dim3((nframes + fpb - 1) / fpb), dim3(DEC_LANES), 0, s, words, nwords, nbytes, nframes,
-                       sp, chn_lanes, fmt, out, out_bytes, info);
+                       sp, chn_lanes, fmt, out, out_bytes, info, ablate_flags());
     return hipGetLastError();
 }
 

@@ -149,6 +149,10 @@ BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uin
                                     const bnflac_stream_params *sp, int out_format, uint8_t *d_out,
                                     uint64_t out_bytes, bnflac_frame_info *d_info, void *hip_stream);
 
+/* Timing experiments only: skip parts of the kernels (bit0 CRC-16, bit1 PCM stores,
+ * bit2 restore, bit3 Rice decode, bit4 subframe walk).  Output is wrong while set. */
+BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags);
+
 /* Bytes of one sample frame (all channels of one sample index) in out_format. */
 BNFLAC_API uint32_t bnflac_out_stride(int out_format, const bnflac_stream_params *sp);
 

@@ -140,11 +140,15 @@ static int br_need(oracle_decoder *d, uint64_t bits) {
     return 1;
 }
 
-static uint32_t br_peek_bits(const oracle_decoder *d, unsigned bits) { /* bits <= 32 */
-    uint64_t v = 0;
-    uint64_t p = d->bitpos;
-    for (unsigned i = 0; i < bits; i++, p++) v = (v << 1) | ((d->buf[p >> 3] >> (7 - (p & 7))) & 1u);
-    return (uint32_t)v;
+/* up to 32 bits at the cursor, MSB first (libFLAC's bitreader works on whole 32-bit
+ * words; this reads the 5 bytes that can hold them).  Bytes past len read as 0: callers
+ * have already checked availability with br_need. */
+static uint32_t br_peek_bits(const oracle_decoder *d, unsigned bits) { /* 1..32 */
+    const uint64_t byte = d->bitpos >> 3;
+    uint64_t w = 0;
+    for (unsigned i = 0; i < 5; i++) w = (w << 8) | (byte + i < d->len ? d->buf[byte + i] : 0u);
+    w <<= 24 + (d->bitpos & 7);           /* cursor bit at bit 63 */
+    return (uint32_t)(w >> (64 - bits));
 }
 
 /* FLAC__bitreader_read_raw_uint32: bits == 0 yields 0. */
@@ -183,14 +187,22 @@ static int br_u64(oracle_decoder *d, uint64_t *v, unsigned bits) {
 static int br_unary(oracle_decoder *d, uint32_t *v) {
     uint32_t n = 0;
     for (;;) {
-        if (!br_need(d, 1)) return 0;
-        uint32_t b = br_peek_bits(d, 1);
-        d->bitpos++;
-        if (b) break;
-        n++;
+        uint64_t avail = (uint64_t)d->len * 8u - d->bitpos;
+        if (avail == 0) {
+            if (!br_need(d, 1)) return 0;
+            continue;
+        }
+        unsigned take = avail >= 32 ? 32u : (unsigned)avail;
+        uint32_t w = br_peek_bits(d, take) << (32 - take);
+        if (w) {
+            unsigned z = (unsigned)__builtin_clz(w);
+            d->bitpos += z + 1;
+            *v = n + z;
+            return 1;
+        }
+        n += take;
+        d->bitpos += take;
     }
-    *v = n;
-    return 1;
 }
 
 /* FLAC__bitreader_read_rice_signed_block: C @0x10001b30 / asm-bswap @0x1001aed0.
@@ -198,6 +210,24 @@ static int br_unary(oracle_decoder *d, uint32_t *v) {
 static int br_rice_block(oracle_decoder *d, int32_t *vals, unsigned n, unsigned k) {
     for (unsigned i = 0; i < n; i++) {
         uint32_t q, lsb;
+        /* fast path: one 64-bit big-endian window holds the whole codeword */
+        if ((uint64_t)d->len * 8u - d->bitpos >= 64) {
+            const uint8_t *p = d->buf + (d->bitpos >> 3);
+            uint64_t w = 0;
+            for (int b = 0; b < 8; b++) w = (w << 8) | p[b];
+            const unsigned sh = (unsigned)(d->bitpos & 7u);
+            w <<= sh;
+            if (w) {
+                const unsigned z = (unsigned)__builtin_clzll(w);
+                if (z + 1u + k <= 64u - sh) {
+                    lsb = k ? (uint32_t)((w << (z + 1)) >> (64 - k)) : 0u;
+                    d->bitpos += z + 1u + k;
+                    const uint32_t u = (k ? ((uint32_t)z << k) : (uint32_t)z) | lsb;
+                    vals[i] = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1u)));
+                    continue;
+                }
+            }
+        }
         if (!br_unary(d, &q)) return 0;
         if (!br_u32(d, &lsb, k)) return 0;
         uint32_t u = (k ? (q << k) : q) | lsb;
@@ -318,15 +348,16 @@ static void lpc_restore_32(const int32_t *res, unsigned n, const int32_t *c, uns
  * count: a negative shift (>= 32 as unsigned) fills with the sign bit. */
 static void lpc_restore_16_mmx(const int32_t *res, unsigned n, const int32_t *c, unsigned order,
                                int shift, int32_t *data) {
+    int32_t hs[FLAC__MAX_LPC_ORDER + 4]; /* scratch: per-tap history words */
     for (unsigned i = 0; i < n; i++) {
         uint32_t sum = 0;
         for (unsigned j = 0; j < order; j++) {
             int idx = (int)i - 1 - (int)j;
-            int32_t h;
-            if (j < 4) h = (idx >= 0) ? trunc16(data[idx]) : sat16(data[idx]);
-            else h = sat16(data[idx]);
-            sum += (uint32_t)((int32_t)(int16_t)c[j] * h);
+            /* taps 0..3 come from mm4: low 16 bits of computed samples, saturated
+             * warm-ups; older taps are reloaded from memory with packssdw */
+            hs[j] = (j < 4 && idx >= 0) ? trunc16(data[idx]) : sat16(data[idx]);
         }
+        for (unsigned j = 0; j < order; j++) sum += (uint32_t)((int32_t)(int16_t)c[j] * hs[j]);
         int32_t sh = ((uint32_t)shift >= 32u) ? ((int32_t)sum >> 31) : ((int32_t)sum >> shift);
         data[i] = (int32_t)((uint32_t)res[i] + (uint32_t)sh);
     }
