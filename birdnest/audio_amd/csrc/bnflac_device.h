@@ -40,7 +40,12 @@ typedef struct {
     uint32_t pad_;
 } bnf_frame_info;
 
-enum { BNF_FL_NEEDS_SLOW = 1u };
+enum {
+    BNF_FL_NEEDS_SLOW = 1u,
+    BNF_FL_OUT_OF_BOUNDS = 2u, /* set by k_decode: frame would end past out_bytes (SKIPPED) */
+    BNF_FL_UNSUPPORTED = 4u,   /* set by k_decode: the output format cannot carry the frame (SKIPPED) */
+    BNF_FL_W32 = 16u           /* set by k_parse: an LPC order > 8 (decoded by k_decode<32>) */
+};
 
 /* Output formats of k_decode */
 enum {

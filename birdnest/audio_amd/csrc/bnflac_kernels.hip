@@ -3,21 +3,30 @@
  *
  * Replaces the arithmetic of libFLAC 1.2.1's read_frame_ (LibFlac.dll@0x100118c0) and
  * everything under it, plus the PCM packing of
- * BirdNest.Audio's write callbacks (A15/A17), with three kernels:
+ * BirdNest.Audio's write callbacks (A15/A17), with these kernels:
  *
  *   k_sync_scan  -- candidate frame syncs: byte p with b[p]==0xFF, b[p+1]>>2==0x3e
  *                   (frame_sync_ @0x10011760's test), ordered compaction.
  *   k_parse      -- one lane per candidate: frame header (read_frame_header_
  *                   @0x10011d70, CRC-8), then walks subframes 0..C-2 to find where
  *                   each subframe starts (the Rice bit cursor is serial per frame).
- *   k_decode     -- one lane per (frame, channel) subframe, 64-lane workgroups:
- *                   partitioned-Rice residuals (A9) into an LDS row, FIXED/LPC restore
- *                   with libFLAC's exact 16-bit-MMX / ia32 / 64-bit dispatch (A7, A8),
+ *   k_decode<W>  -- one lane per (frame, channel) subframe, 64-lane workgroups:
+ *                   partitioned-Rice residuals (A9) fused with the FIXED/LPC restore
+ *                   (libFLAC's exact 16-bit-MMX / ia32 / 64-bit dispatch, A7, A8) and
  *                   wasted bits (A5); then the workgroup decorrelates (A12) and writes
- *                   the requested PCM layout with coalesced stores; the last-channel
- *                   lanes check zero padding and the frame CRC-16 (A4, A11).
+ *                   the requested PCM layout with coalesced stores; the channel lanes
+ *                   of a frame check zero padding and the frame CRC-16 (A4, A11).
+ *                   W = 8 serves frames whose LPC orders are all <= 8 (register ring
+ *                   of 8, low VGPR count); W = 32 the rest.
  *
- * Integer-only, HBM/latency bound; no MFMA.  Bit-exactness is defined
+ * Bit reader.  Every lane owns an 8-slot ring of 16-byte blocks of its own bitstream in
+ * LDS, filled by exec-masked LDS-DMA (global_load_lds_dwordx4) once per 32-sample
+ * chunk; a chunk decodes from blocks that landed during the previous chunk, so HBM
+ * latency is hidden behind a whole chunk of work and the per-codeword cursor advance
+ * is branch-free (one ds_read_b32).  Words outside the landed range are read from
+ * global memory directly (rare: jumps, very high bit rates).
+ *
+ * Integer-only, HBM/issue bound; no MFMA.  Bit-exactness is defined
  * by oracle/flac_oracle.c, which restates the same DLL behaviour on the CPU.
  */
 #include <hip/hip_runtime.h>
@@ -34,39 +43,100 @@ __constant__ uint8_t g_crc8_tab[256];
 __constant__ uint16_t g_crc16_tab[8][256]; /* slice-by-8 */
 __constant__ uint16_t g_crc16_xpow[40];    /* x^(8*2^j) mod P for j < 40 */
 
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gvoid;
+
 /* ----------------------------------------------------------------- bit reader */
-/* MSB-first bit stream over little-endian 32-bit words.  A 64-bit window (hi:lo)
- * plus one prefetched word; `off` is the bit offset of the cursor inside hi. */
+#define RING 8            /* 16-byte slots per lane */
+#define RING_LANE_DW 256  /* dwords per slot row (64 lanes x 4) */
+#define RING_DW (RING * RING_LANE_DW)
+
+/* MSB-first bit stream.  Window hi:lo (big-endian words) with the cursor `off` bits
+ * into hi; nx = word `wi` (the next to enter the window). */
 struct BR {
-    const uint32_t *__restrict__ w;
-    uint32_t nw;
-    uint32_t wi;
-    uint32_t off;
-    uint32_t hi, lo, nx;
+    const uint32_t *__restrict__ w; /* stream words (16-byte aligned base) */
+    uint32_t nw;                    /* words readable (allocation covers nblk*4) */
+    uint32_t nblk;                  /* 16-byte blocks readable */
+    lds_u32 *ring;                  /* slot 0 of lane 0 (wave-uniform) */
+    lds_u32 *lring;                 /* this lane's slot-0 entry */
+    uint32_t wi, off, hi, lo, nx;
+    uint32_t vend, iend;            /* blocks < vend landed in the ring; < iend issued */
 };
 
-DEV uint32_t ldw(const uint32_t *__restrict__ w, uint32_t nw, uint32_t i) {
-    return i < nw ? __builtin_bswap32(w[i]) : 0u;
+DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, uint32_t lane) {
+    b.w = words;
+    b.nblk = (uint32_t)((nbytes + 15u) >> 4);
+    b.nw = b.nblk * 4u;
+    b.ring = ring;
+    b.lring = ring + lane * 4u;
+    b.wi = b.off = b.hi = b.lo = b.nx = 0;
+    b.vend = b.iend = 0;
 }
-DEV void br_seek(BR &b, uint64_t bit) {
-    b.wi = (uint32_t)(bit >> 5);
-    b.off = (uint32_t)(bit & 31u);
-    b.hi = ldw(b.w, b.nw, b.wi);
-    b.lo = ldw(b.w, b.nw, b.wi + 1);
-    b.nx = ldw(b.w, b.nw, b.wi + 2);
+
+DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+DEV uint32_t br_word(const BR &b, uint32_t w) {
+    uint32_t v = b.lring[((w & 0x1cu) << 6) + (w & 3u)];
+    if ((w >> 2) >= b.vend) v = (w < b.nw) ? b.w[w] : 0u; /* not landed: read HBM directly */
+    return __builtin_bswap32(v);
 }
-DEV uint64_t br_pos(const BR &b) { return ((uint64_t)b.wi << 5) + b.off; }
-DEV uint32_t br_peek(const BR &b) { return __funnelshift_l(b.lo, b.hi, b.off); }
-DEV void br_adv(BR &b, uint32_t n) { /* n <= 32 */
-    uint32_t o = b.off + n;
-    if (o >= 32u) {
-        b.hi = b.lo;
-        b.lo = b.nx;
-        b.wi++;
-        b.nx = ldw(b.w, b.nw, b.wi + 2);
-        o -= 32u;
+
+/* Issue the blocks this lane will need next (exec-masked LDS-DMA per ring slot).
+ * Everything issued earlier has landed once the wait returns. */
+DEV void br_refill(BR &b) {
+    wait_vm();
+    b.vend = b.iend;
+    const uint32_t need = b.wi >> 2; /* br_adv re-reads word wi: keep its block */
+    const uint32_t lo = max(b.iend, need), hi = need + RING;
+#pragma unroll
+    for (int s = 0; s < RING; s++) {
+        const uint32_t j = lo + (((uint32_t)s - lo) & (RING - 1u));
+        if (j < hi) {
+            const uint32_t jj = min(j, b.nblk - 1u);
+            __builtin_amdgcn_global_load_lds((gvoid *)(b.w + (uint64_t)jj * 4u), (lds_void *)(b.ring + s * RING_LANE_DW),
+                                             16, 0, 0);
+        }
     }
-    b.off = o;
+    b.iend = hi;
+}
+
+/* Blocking seek: fill the ring from the block holding `bit`, then load the window. */
+DEV void br_seek(BR &b, uint64_t bit) {
+    const uint32_t w = (uint32_t)(bit >> 5);
+    b.off = (uint32_t)(bit & 31u);
+    b.wi = w; /* refill starts at block w>>2 */
+    b.iend = b.vend = w >> 2;
+    br_refill(b);
+    wait_vm();
+    b.vend = b.iend;
+    b.hi = br_word(b, w);
+    b.lo = br_word(b, w + 1u);
+    b.nx = br_word(b, w + 2u);
+    b.wi = w + 2u;
+}
+
+/* Non-blocking jump forward (skips); words not yet in the ring come from HBM. */
+DEV void br_jump(BR &b, uint64_t bit) {
+    const uint32_t w = (uint32_t)(bit >> 5);
+    b.off = (uint32_t)(bit & 31u);
+    b.hi = br_word(b, w);
+    b.lo = br_word(b, w + 1u);
+    b.nx = br_word(b, w + 2u);
+    b.wi = w + 2u;
+}
+
+DEV uint64_t br_pos(const BR &b) { return ((uint64_t)(b.wi - 2u) << 5) + b.off; }
+DEV uint32_t br_peek(const BR &b) { return __funnelshift_l(b.lo, b.hi, b.off); }
+DEV void br_adv(BR &b, uint32_t n) { /* n <= 32; branch-free */
+    const uint32_t o = b.off + n;
+    const bool c = o >= 32u;
+    b.hi = c ? b.lo : b.hi;
+    b.lo = c ? b.nx : b.lo;
+    b.off = o & 31u;
+    b.wi += c ? 1u : 0u;
+    b.nx = br_word(b, b.wi);
 }
 DEV uint32_t br_read(BR &b, uint32_t n) { /* 0..32 bits */
     uint32_t v = n ? (br_peek(b) >> ((32u - n) & 31u)) : 0u;
@@ -80,7 +150,7 @@ DEV int32_t br_read_s(BR &b, uint32_t n) {
 }
 DEV void br_skip(BR &b, uint64_t n) {
     if (n <= 32) br_adv(b, (uint32_t)n);
-    else br_seek(b, br_pos(b) + n);
+    else br_jump(b, br_pos(b) + n);
 }
 /* count zeros up to and including the terminating 1 (read_unary_unsigned @0x10001960) */
 DEV bool br_unary(BR &b, uint32_t &q, uint64_t limit) {
@@ -350,23 +420,27 @@ DEV uint32_t parse_subframe_head(BR &b, uint32_t bps, uint32_t bs, uint64_t limi
     return br_pos(b) > limit ? BNF_ST_TRUNC : BNF_ST_OK;
 }
 
-/* Skip the residual of a FIXED/LPC subframe (k_parse's cursor walk). */
-DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit) {
+/* Skip the residual of a FIXED/LPC subframe (k_parse's cursor walk).  The ring is
+ * refilled every 32 codewords (lanes of a wave stay in step on regular streams). */
+DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate) {
     const uint32_t parts = 1u << h.porder;
     const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
     const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
+    uint32_t since = 0;
     for (uint32_t p = 0; p < parts; p++) {
-        uint32_t k = br_read(b, plen);
-        uint32_t cnt = (h.porder == 0 || p > 0) ? psamples : psamples - h.order;
+        const uint32_t k = br_read(b, plen);
+        const uint32_t cnt = (h.porder == 0 || p > 0) ? psamples : psamples - h.order;
         if (k >= pesc) {
-            uint32_t nb = br_read(b, 5);
+            const uint32_t nb = br_read(b, 5);
             br_skip(b, (uint64_t)nb * cnt);
         } else {
+            const uint32_t k1 = k + 1u;
             for (uint32_t i = 0; i < cnt; i++) {
-                uint32_t w = br_peek(b);
-                uint32_t q = w ? (uint32_t)__builtin_clz(w) : 32u;
-                if (q + 1u + k <= 32u) {
-                    br_adv(b, q + 1u + k);
+                if ((since++ & 31u) == 0 && !(ablate & 32u)) br_refill(b);
+                const uint32_t w = br_peek(b);
+                const uint32_t q = w ? (uint32_t)__builtin_clz(w) : 32u;
+                if (q + k1 <= 32u) {
+                    br_adv(b, q + k1);
                 } else {
                     uint32_t qq;
                     if (!br_unary(b, qq, limit)) return BNF_ST_TRUNC;
@@ -464,12 +538,14 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 }
 
 /* ==================================================================== k_parse */
-/* One lane per candidate frame: header + cursor walk over subframes 0..C-2. */
-__global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint32_t nwords, uint64_t nbytes,
+/* One lane per candidate frame: header + cursor walk over subframes 0..C-2.  Also
+ * flags frames with an LPC order above 8 (they go to k_decode<32>). */
+__global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint64_t nbytes,
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
                                               uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate) {
-    uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ uint32_t ring[RING_DW];
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
     bnf_frame_info fi;
     fi.status = BNF_ST_OK;
@@ -489,8 +565,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     const uint64_t limit = nbytes * 8u;
     const uint64_t fbit = fi.frame_off * 8u;
     BR b;
-    b.w = words;
-    b.nw = nwords;
+    br_init(b, words, nbytes, (lds_u32 *)ring, threadIdx.x);
     uint32_t st = parse_header(b, fbit, limit, sp, fi);
     if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
     if (st == BNF_ST_OK) {
@@ -500,17 +575,24 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
         else if (sp.has_stream_info && sp.min_blocksize == sp.max_blocksize) sample = (uint64_t)sp.min_blocksize * fi.number;
         else sample = (uint64_t)fi.blocksize * fi.number;
         fi.out_sample = out_sample_in ? out_sample_in[f] : sample - base_sample;
+        uint32_t maxorder = 0;
         for (uint32_t ch = 0; ch < fi.channels; ch++) {
             fi.sub_start[ch] = (uint32_t)(br_pos(b) - fbit);
-            if (ch + 1 == fi.channels) break; /* the last subframe is walked by k_decode */
+            if (ch + 1 == fi.channels) {
+                /* the last subframe is walked by k_decode; only peek at its type byte */
+                const uint32_t x = br_peek(b) >> 24;
+                if (!(x & 0x80u) && (x & 0x7Eu) >= 0x40u) maxorder = max(maxorder, ((x >> 1) & 31u) + 1u);
+                break;
+            }
             if (ablate & 16u) { fi.sub_start[ch + 1] = fi.sub_start[ch]; continue; }
             SubHdr h;
             int32_t err = -1;
             uint32_t bps = sub_bps(fi, ch);
             st = parse_subframe_head<false>(b, bps, fi.blocksize, limit, h, nullptr, nullptr, err);
             if (st == BNF_ST_OK) {
+                if (h.type == T_LPC) maxorder = max(maxorder, h.order);
                 if (h.type == T_VERB) br_skip(b, (uint64_t)h.bps * fi.blocksize);
-                else if (h.type == T_FIXED || h.type == T_LPC) st = skip_residual(b, h, fi.blocksize, limit);
+                else if (h.type == T_FIXED || h.type == T_LPC) st = skip_residual(b, h, fi.blocksize, limit, ablate);
                 if (st == BNF_ST_OK && br_pos(b) > limit) st = BNF_ST_TRUNC;
             }
             if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
@@ -522,6 +604,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
                 break;
             }
         }
+        if (maxorder > 8) fi.flags |= BNF_FL_W32;
     }
     fi.status = st;
     info[f] = fi;
@@ -537,27 +620,24 @@ struct RS { /* residual reader state */
     uint32_t k, esc, left, pidx, nparts, psamples, order, plen, pesc, porder;
 };
 
-/* next residual (read_residual_partitioned_rice_ @0x10012da0 with the Rice block reader
- * @0x10001b30/@0x1001aed0: u = (q << k) | lsb in 32-bit unsigned, zig-zag). */
-DEV int32_t next_val(BR &b, RS &s, uint64_t limit, uint32_t &trunc) {
-    if (s.verb) return br_read_s(b, s.k);
-    while (s.left == 0) {
-        if (s.pidx >= s.nparts) { trunc = 1; return 0; }
-        uint32_t kk = br_read(b, s.plen);
-        s.left = (s.porder == 0 || s.pidx > 0) ? s.psamples : s.psamples - s.order;
-        if (kk < s.pesc) {
-            s.k = kk;
-            s.esc = 0;
-        } else {
-            s.k = br_read(b, 5);
-            s.esc = 1;
-        }
-        s.pidx++;
+/* Rice partition header (read_residual_partitioned_rice_ @0x10012da0) */
+DEV void read_partition(BR &b, RS &s) {
+    const uint32_t kk = br_read(b, s.plen);
+    s.left = (s.porder == 0 || s.pidx > 0) ? s.psamples : s.psamples - s.order;
+    if (kk < s.pesc) {
+        s.k = kk;
+        s.esc = 0;
+    } else {
+        s.k = br_read(b, 5);
+        s.esc = 1;
     }
-    s.left--;
-    if (s.esc) return br_read_s(b, s.k);
-    const uint32_t k = s.k;
-    uint32_t w = br_peek(b);
+    s.pidx++;
+}
+
+/* One Rice codeword (the block reader @0x10001b30/@0x1001aed0: u = (q << k) | lsb in
+ * 32-bit unsigned, zig-zag). */
+DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc) {
+    const uint32_t w = br_peek(b);
     uint32_t q = w ? (uint32_t)__builtin_clz(w) : 32u;
     uint32_t lsb;
     if (q + 1u + k <= 32u) {
@@ -567,8 +647,20 @@ DEV int32_t next_val(BR &b, RS &s, uint64_t limit, uint32_t &trunc) {
         if (!br_unary(b, q, limit)) trunc = 1;
         lsb = br_read(b, k);
     }
-    uint32_t u = (k ? (q << k) : q) | lsb;
+    const uint32_t u = (q << k) | lsb;
     return (int32_t)((u >> 1) ^ (0u - (u & 1u)));
+}
+
+/* next residual of the generic path */
+DEV int32_t next_val(BR &b, RS &s, uint64_t limit, uint32_t &trunc) {
+    if (s.verb) return br_read_s(b, s.k);
+    while (s.left == 0) {
+        if (s.pidx >= s.nparts) { trunc = 1; return 0; }
+        read_partition(b, s);
+    }
+    s.left--;
+    if (s.esc) return br_read_s(b, s.k);
+    return rice_one(b, s.k, limit, trunc);
 }
 
 DEV void finish_partitions(BR &b, RS &s) {
@@ -584,104 +676,164 @@ DEV int32_t sat16(int32_t x) { return min(max(x, -32768), 32767); }
 DEV int32_t tr16(int32_t x) { return (int32_t)(int16_t)(uint16_t)(uint32_t)x; }
 DEV int32_t mul24(int32_t a, int32_t b) { return ((a << 8) >> 8) * ((b << 8) >> 8); }
 
-/* LPC restore of one 32-sample chunk (rows hold residuals on entry, samples << wasted
- * on exit).  W: register ring size (order <= W); P: libFLAC restore path. */
-template <int W, int P>
-DEV void lpc_chunk(int32_t *row, int32_t (&c)[32], int32_t (&h)[32], int32_t (&ht)[4], uint32_t n0,
-                   uint32_t nvalid, uint32_t order, int32_t shift, uint32_t wasted) {
+/* LPC prediction for the sample at ring position i (compile-time), libFLAC path P.
+ * sh is the path's effective shift (MMX psrad: >= 32 -> 31; ia32 sar: & 31; 64-bit
+ * _allshr: & 0xFF, >= 64 -> 63). */
+template <int W, int P, int N>
+DEV int32_t lpc_pred(const int32_t (&c)[N], const int32_t (&h)[N], const int32_t (&ht)[4], int i, int32_t sh) {
+    if (P == P_MMX16) {
+        int32_t sum = 0;
+#pragma unroll
+        for (int t = 0; t < W; t++) {
+            const int32_t hv = (t < 4) ? ht[(i - 1 - t) & 3] : h[((i - 1 - t) % W + W) % W];
+            sum += mul24(c[t], hv);
+        }
+        return sum >> sh;
+    } else if (P == P_IA32) {
+        /* exact int32 wrap product via 12-bit split: c*s = (c*(s>>12) << 12) + c*(s&0xfff) */
+        int32_t shi = 0, slo = 0;
+#pragma unroll
+        for (int t = 0; t < W; t++) {
+            const int32_t hv = h[((i - 1 - t) % W + W) % W];
+            shi += mul24(c[t], hv >> 12);
+            slo += mul24(c[t], hv & 0xfff);
+        }
+        const int32_t sum = (int32_t)(((uint32_t)shi << 12) + (uint32_t)slo);
+        return sum >> sh;
+    } else {
+        int64_t sum = 0;
+#pragma unroll
+        for (int t = 0; t < W; t++) sum += (int64_t)c[t] * (int64_t)h[((i - 1 - t) % W + W) % W];
+        return (int32_t)(sum >> sh);
+    }
+}
+
+template <int W, int P, int N>
+DEV void lpc_push(int32_t (&h)[N], int32_t (&ht)[4], int i, int32_t s) {
+    if (P == P_MMX16) {
+        ht[i & 3] = tr16(s);
+        h[i % W] = sat16(s);
+    } else {
+        h[i % W] = s;
+    }
+}
+
+/* Generic LPC restore of one chunk (rows hold residuals on entry, samples << wasted on
+ * exit); handles warm-up samples and short chunks. */
+template <int W, int P, int N>
+DEV void lpc_chunk(int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4], uint32_t n0,
+                   uint32_t nvalid, uint32_t order, int32_t sh, uint32_t wasted) {
 #pragma unroll
     for (int i = 0; i < CHUNK; i++) {
-        const int slot = i % W;
         const uint32_t n = n0 + (uint32_t)i;
         if ((uint32_t)i < nvalid) {
             int32_t s;
             if (n < order) {
-                s = h[slot];
+                s = h[i % W];
                 if (P == P_MMX16) s = row[i]; /* raw warm-up kept in the row */
             } else {
-                const int32_t r = row[i];
-                int32_t pred;
-                if (P == P_MMX16) {
-                    int32_t sum = 0;
-#pragma unroll
-                    for (int t = 0; t < W; t++) {
-                        const int32_t hv = (t < 4) ? ht[(i - 1 - t) & 3] : h[((i - 1 - t) % W + W) % W];
-                        sum += mul24(c[t], hv);
-                    }
-                    pred = ((uint32_t)shift >= 32u) ? (sum >> 31) : (sum >> shift);
-                } else if (P == P_IA32) {
-                    /* exact int32 wrap product via 12-bit split: c*s = (c*(s>>12) << 12) + c*(s&0xfff) */
-                    int32_t shi = 0, slo = 0;
-#pragma unroll
-                    for (int t = 0; t < W; t++) {
-                        const int32_t hv = h[((i - 1 - t) % W + W) % W];
-                        shi += mul24(c[t], hv >> 12);
-                        slo += mul24(c[t], hv & 0xfff);
-                    }
-                    const int32_t sum = (int32_t)(((uint32_t)shi << 12) + (uint32_t)slo);
-                    pred = sum >> (shift & 31);
-                } else {
-                    int64_t sum = 0;
-#pragma unroll
-                    for (int t = 0; t < W; t++) sum += (int64_t)c[t] * (int64_t)h[((i - 1 - t) % W + W) % W];
-                    const uint32_t cnt = (uint32_t)shift & 0xFFu;
-                    pred = (cnt >= 64u) ? (int32_t)(sum >> 63) : (int32_t)(sum >> cnt);
-                }
-                s = (int32_t)((uint32_t)r + (uint32_t)pred);
+                s = (int32_t)((uint32_t)row[i] + (uint32_t)lpc_pred<W, P>(c, h, ht, i, sh));
+                if (P == P_MMX16) ht[i & 3] = tr16(s);
             }
-            if (P == P_MMX16) {
-                if (n >= order) ht[i & 3] = tr16(s);
-                h[slot] = sat16(s);
-            } else {
-                h[slot] = s;
-            }
+            if (P == P_MMX16) h[i % W] = sat16(s);
+            else h[i % W] = s;
             row[i] = (int32_t)((uint32_t)s << wasted);
         }
     }
 }
 
-/* FLAC__fixed_restore_signal @0x10003810 over one chunk (ring of 8, 32-bit wrap) */
-DEV void fixed_chunk(int32_t *row, int32_t (&h)[32], uint32_t n0, uint32_t nvalid, uint32_t order, uint32_t wasted) {
+/* Fused Rice decode + LPC restore of a full chunk past the warm-up, inside one Rice
+ * partition (parameter k, not escaped): the residual never leaves registers and the
+ * two dependency chains (bit cursor, predictor) interleave. */
+template <int W, int P, int N>
+DEV void lpc_fused(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
+                   int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc) {
+#pragma unroll 1
+    for (int j = 0; j < CHUNK; j += W) {
+#pragma unroll
+        for (int t = 0; t < W; t++) {
+            const int32_t r = rice_one(b, k, limit, trunc);
+            const int32_t s = (int32_t)((uint32_t)r + (uint32_t)lpc_pred<W, P>(c, h, ht, t, sh));
+            lpc_push<W, P>(h, ht, t, s);
+            row[j + t] = (int32_t)((uint32_t)s << wasted);
+        }
+    }
+}
+
+/* FLAC__fixed_restore_signal @0x10003810 (ring of 8, 32-bit wrap) */
+template <int N>
+DEV uint32_t fixed_pred(const int32_t (&h)[N], int i, uint32_t order) {
+    const uint32_t a = (uint32_t)h[(i - 1) & 7], bb = (uint32_t)h[(i - 2) & 7], c = (uint32_t)h[(i - 3) & 7],
+                   d = (uint32_t)h[(i - 4) & 7];
+    switch (order) {
+    case 0: return 0;
+    case 1: return a;
+    case 2: return (a << 1) - bb;
+    case 3: return (((a - bb) << 1) + (a - bb)) + c;
+    default: return ((a + c) << 2) - ((bb << 2) + (bb << 1)) - d;
+    }
+}
+
+template <int N>
+DEV void fixed_chunk(int32_t *row, int32_t (&h)[N], uint32_t n0, uint32_t nvalid, uint32_t order, uint32_t wasted) {
 #pragma unroll
     for (int i = 0; i < CHUNK; i++) {
         const uint32_t n = n0 + (uint32_t)i;
         if ((uint32_t)i < nvalid) {
             uint32_t s;
-            if (n < order) {
-                s = (uint32_t)h[i & 7];
-            } else {
-                const uint32_t r = (uint32_t)row[i];
-                const uint32_t a = (uint32_t)h[(i - 1) & 7], bb = (uint32_t)h[(i - 2) & 7], c = (uint32_t)h[(i - 3) & 7],
-                               d = (uint32_t)h[(i - 4) & 7];
-                switch (order) {
-                case 0: s = r; break;
-                case 1: s = r + a; break;
-                case 2: s = r + (a << 1) - bb; break;
-                case 3: s = r + (((a - bb) << 1) + (a - bb)) + c; break;
-                default: s = r + ((a + c) << 2) - ((bb << 2) + (bb << 1)) - d; break;
-                }
-            }
+            if (n < order) s = (uint32_t)h[i & 7];
+            else s = (uint32_t)row[i] + fixed_pred(h, i, order);
             h[i & 7] = (int32_t)s;
             row[i] = (int32_t)(s << wasted);
         }
     }
 }
 
-/* CRC-16 (poly 0x8005) over bytes [b0, b1) of the word-addressed stream, slice-by-8 */
-DEV uint32_t crc16_range(const uint32_t *__restrict__ words, uint32_t nw, uint64_t b0, uint64_t b1) {
+template <int N>
+DEV void fixed_fused(BR &b, uint32_t k, int32_t *row, int32_t (&h)[N], uint32_t order, uint32_t wasted,
+                     uint64_t limit, uint32_t &trunc) {
+#pragma unroll 1
+    for (int j = 0; j < CHUNK; j += 8) {
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const uint32_t s = (uint32_t)rice_one(b, k, limit, trunc) + fixed_pred(h, t, order);
+            h[t] = (int32_t)s;
+            row[j + t] = (int32_t)(s << wasted);
+        }
+    }
+}
+
+/* CRC-16 (poly 0x8005) over bytes [b0, b1), slice-by-8 with the tables in LDS. */
+DEV uint32_t crc16_step8(uint32_t crc, uint32_t w0, uint32_t w1, const lds_u16 *T) {
+    const uint32_t a = w0 ^ (crc << 16);
+    return T[7 * 256 + (a >> 24)] ^ T[6 * 256 + ((a >> 16) & 0xff)] ^ T[5 * 256 + ((a >> 8) & 0xff)] ^
+           T[4 * 256 + (a & 0xff)] ^ T[3 * 256 + (w1 >> 24)] ^ T[2 * 256 + ((w1 >> 16) & 0xff)] ^
+           T[1 * 256 + ((w1 >> 8) & 0xff)] ^ T[w1 & 0xff];
+}
+DEV uint32_t crc16_range(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
     uint32_t crc = 0;
     uint64_t p = b0;
-    const uint8_t *bytes = (const uint8_t *)words;
-    while (p < b1 && (p & 7u)) { crc = ((crc << 8) ^ g_crc16_tab[0][((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
-    while (p + 8 <= b1) {
-        const uint32_t w0 = ldw(words, nw, (uint32_t)(p >> 2)), w1 = ldw(words, nw, (uint32_t)(p >> 2) + 1);
-        const uint32_t a = w0 ^ (crc << 16);
-        crc = g_crc16_tab[7][a >> 24] ^ g_crc16_tab[6][(a >> 16) & 0xff] ^ g_crc16_tab[5][(a >> 8) & 0xff] ^
-              g_crc16_tab[4][a & 0xff] ^ g_crc16_tab[3][w1 >> 24] ^ g_crc16_tab[2][(w1 >> 16) & 0xff] ^
-              g_crc16_tab[1][(w1 >> 8) & 0xff] ^ g_crc16_tab[0][w1 & 0xff];
-        p += 8;
+    while (p < b1 && (p & 15u)) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
+    const uint4 *q = (const uint4 *)(bytes + p);
+    const uint32_t nq = (uint32_t)((b1 - p) >> 4);
+    uint32_t i = 0;
+    for (; i + 4 <= nq; i += 4) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = q[i + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            crc = crc16_step8(crc, __builtin_bswap32(v[u].x), __builtin_bswap32(v[u].y), T);
+            crc = crc16_step8(crc, __builtin_bswap32(v[u].z), __builtin_bswap32(v[u].w), T);
+        }
     }
-    while (p < b1) { crc = ((crc << 8) ^ g_crc16_tab[0][((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
+    for (; i < nq; i++) {
+        const uint4 v = q[i];
+        crc = crc16_step8(crc, __builtin_bswap32(v.x), __builtin_bswap32(v.y), T);
+        crc = crc16_step8(crc, __builtin_bswap32(v.z), __builtin_bswap32(v.w), T);
+    }
+    p += (uint64_t)nq * 16u;
+    while (p < b1) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
     return crc;
 }
 
@@ -752,10 +904,29 @@ DEV void pack_chunk(const int32_t *lds, uint32_t lane, uint32_t fpb, uint32_t ch
     }
 }
 
-__global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict__ words, uint32_t nwords, uint64_t nbytes,
+#define LPC_DISPATCH(FN, W_, ...)                                                                   \
+    do {                                                                                             \
+        if (h.path == P_MMX16) {                                                                     \
+            if (W_ == 8) FN<8, P_MMX16>(__VA_ARGS__);                                                \
+            else if (MAXW >= 16 && W_ == 16) FN<(MAXW >= 16 ? 16 : 8), P_MMX16>(__VA_ARGS__);        \
+            else if (MAXW >= 32) FN<(MAXW >= 32 ? 32 : 8), P_MMX16>(__VA_ARGS__);                    \
+        } else if (h.path == P_IA32) {                                                               \
+            if (W_ == 8) FN<8, P_IA32>(__VA_ARGS__);                                                 \
+            else if (MAXW >= 16 && W_ == 16) FN<(MAXW >= 16 ? 16 : 8), P_IA32>(__VA_ARGS__);         \
+            else if (MAXW >= 32) FN<(MAXW >= 32 ? 32 : 8), P_IA32>(__VA_ARGS__);                     \
+        } else {                                                                                     \
+            if (W_ == 8) FN<8, P_WIDE>(__VA_ARGS__);                                                 \
+            else if (MAXW >= 16 && W_ == 16) FN<(MAXW >= 16 ? 16 : 8), P_WIDE>(__VA_ARGS__);         \
+            else if (MAXW >= 32) FN<(MAXW >= 32 ? 32 : 8), P_WIDE>(__VA_ARGS__);                     \
+        }                                                                                            \
+    } while (0)
+
+template <int MAXW>
+__global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
                                                       uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                       int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
                                                       bnf_frame_info *__restrict__ info, uint32_t ablate) {
+    __shared__ uint32_t ring[RING_DW];
     __shared__ int32_t lds[DEC_LANES * ROW];
     __shared__ uint32_t f_bs[DEC_LANES], f_ch[DEC_LANES], f_as[DEC_LANES], f_ok[DEC_LANES];
     __shared__ uint64_t f_out[DEC_LANES];
@@ -771,6 +942,9 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
     bool have = (fl < fpb) && (f < nframes);
     if (have) fi = info[f];
     const bool frame_ok = have && fi.status == BNF_ST_OK;
+    /* one wave per workgroup: the W=8 and W=32 instances split the blocks between them */
+    if ((MAXW == 32) != (__any(frame_ok && (fi.flags & BNF_FL_W32)) != 0)) return;
+
     bool active = frame_ok && ch < fi.channels && fi.channels <= chn_lanes;
     if (lane < fpb) { f_ok[lane] = 0; f_bad[lane] = 0; f_bs[lane] = 0; }
     __syncthreads();
@@ -817,44 +991,51 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
 
     /* ---- subframe setup */
     BR b;
-    b.w = words;
-    b.nw = nwords;
+    br_init(b, words, nbytes, (lds_u32 *)ring, lane);
     SubHdr h;
     h.type = T_CONST; h.order = 0; h.wasted = 0; h.bps = 0; h.shift = 0; h.path = P_IA32; h.cval = 0;
+    h.porder = 0; h.rice2 = 0;
     RS rs;
     rs.verb = 0; rs.k = 0; rs.esc = 0; rs.left = 0; rs.pidx = 0; rs.nparts = 0; rs.psamples = 0;
     rs.order = 0; rs.plen = 4; rs.pesc = 15; rs.porder = 0;
-    int32_t c[32], hh[32], ht[4];
+    int32_t c[MAXW], hh[MAXW], ht[4];
 #pragma unroll
-    for (int t = 0; t < 32; t++) { c[t] = 0; hh[t] = 0; }
+    for (int t = 0; t < MAXW; t++) { c[t] = 0; hh[t] = 0; }
 #pragma unroll
     for (int t = 0; t < 4; t++) ht[t] = 0;
     uint32_t trunc = 0, st = BNF_ST_OK;
     int32_t err = -1;
     uint32_t bs = 0;
+    int32_t sh = 0;
+    bool fast_ok = false;
     int32_t *row = lds + lane * ROW;
     if (active) {
         bs = fi.blocksize;
         br_seek(b, fi.frame_off * 8u + fi.sub_start[ch]);
         int32_t warm[32], coef[32];
         st = parse_subframe_head<true>(b, sub_bps(fi, ch), bs, limit, h, warm, coef, err);
+        if (st == BNF_ST_OK && h.type == T_LPC && h.order > MAXW) {
+            st = BNF_ST_ERROR; /* k_parse mis-flagged: cannot happen for the subframes it read */
+            err = E_UNPARSEABLE;
+        }
         if (st == BNF_ST_OK) {
             /* coefficients / history into registers (compile-time indices only) */
 #pragma unroll
-            for (int t = 0; t < 32; t++) {
+            for (int t = 0; t < MAXW; t++) {
                 const bool in = (uint32_t)t < h.order;
                 c[t] = (in && h.type == T_LPC) ? coef[t] : 0;
                 const int32_t wv = in ? warm[t] : 0;
                 hh[t] = (h.type == T_LPC && h.path == P_MMX16) ? sat16(wv) : wv;
             }
-            if (h.type == T_FIXED) {
-#pragma unroll
-                for (int t = 0; t < 8; t++) hh[t] = ((uint32_t)t < h.order) ? warm[t] : 0;
-            }
             if (h.type == T_LPC && h.path == P_MMX16) {
 #pragma unroll
-                for (int t = 0; t < 32; t++)
+                for (int t = 0; t < MAXW; t++)
                     if ((uint32_t)t < h.order && (uint32_t)t + 4u >= h.order) ht[t & 3] = sat16(warm[t]);
+            }
+            if (h.type == T_LPC) {
+                if (h.path == P_MMX16) sh = ((uint32_t)h.shift >= 32u) ? 31 : h.shift;
+                else if (h.path == P_IA32) sh = h.shift & 31;
+                else sh = min((uint32_t)h.shift & 0xFFu, 63u);
             }
             rs.verb = (h.type == T_VERB);
             rs.k = h.bps;
@@ -864,6 +1045,8 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
             rs.psamples = h.porder ? bs >> h.porder : bs - h.order;
             rs.plen = h.rice2 ? 5u : 4u;
             rs.pesc = h.rice2 ? 31u : 15u;
+            fast_ok = (h.type == T_FIXED || h.type == T_LPC) && (h.porder == 0 || (rs.psamples % CHUNK) == 0) &&
+                      !(ablate & 12u);
             /* MMX path keeps raw warm-ups for output: stash them in the rows of chunk 0 */
             if (h.type == T_LPC && h.path == P_MMX16) {
                 for (uint32_t t = 0; t < h.order; t++) row[t] = warm[t];
@@ -879,38 +1062,41 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
     const uint32_t nchunks = (mybs + CHUNK - 1) / CHUNK;
     const uint32_t W = h.order <= 8 ? 8u : (h.order <= 16 ? 16u : 32u);
 
-    for (uint32_t k = 0; k < nchunks; k++) {
-        const uint32_t n0 = k * CHUNK;
+    for (uint32_t kc = 0; kc < nchunks; kc++) {
+        const uint32_t n0 = kc * CHUNK;
         const uint32_t nvalid = (active && n0 < bs) ? min((uint32_t)CHUNK, bs - n0) : 0u;
         if (nvalid) {
-            if (h.type == T_FIXED || h.type == T_LPC || h.type == T_VERB) {
-                const uint32_t i0 = (n0 < h.order) ? h.order - n0 : 0u;
-                if (ablate & 8u) {
-                    for (uint32_t i = i0; i < nvalid; i++) row[i] = (int32_t)i;
-                } else {
-                    for (uint32_t i = i0; i < nvalid; i++) row[i] = next_val(b, rs, limit, trunc);
-                }
+            if (h.type != T_CONST) br_refill(b);
+            bool fast = fast_ok && nvalid == CHUNK && n0 >= h.order;
+            if (fast && rs.left == 0) {
+                if (rs.pidx < rs.nparts) read_partition(b, rs);
+                else fast = false;
             }
-            if (ablate & 4u) {
-                /* restore skipped (timing ablation) */
-            } else if (h.type == T_CONST) {
-                for (uint32_t i = 0; i < nvalid; i++) row[i] = (int32_t)((uint32_t)h.cval << h.wasted);
-            } else if (h.type == T_VERB) {
-                for (uint32_t i = 0; i < nvalid; i++) row[i] = (int32_t)((uint32_t)row[i] << h.wasted);
-            } else if (h.type == T_FIXED) {
-                fixed_chunk(row, hh, n0, nvalid, h.order, h.wasted);
-            } else if (h.path == P_MMX16) {
-                if (W == 8) lpc_chunk<8, P_MMX16>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
-                else if (W == 16) lpc_chunk<16, P_MMX16>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
-                else lpc_chunk<32, P_MMX16>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
-            } else if (h.path == P_IA32) {
-                if (W == 8) lpc_chunk<8, P_IA32>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
-                else if (W == 16) lpc_chunk<16, P_IA32>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
-                else lpc_chunk<32, P_IA32>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
+            fast = fast && !rs.esc && rs.left >= CHUNK;
+            if (fast) {
+                if (h.type == T_FIXED) fixed_fused(b, rs.k, row, hh, h.order, h.wasted, limit, trunc);
+                else LPC_DISPATCH(lpc_fused, W, b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
+                rs.left -= CHUNK;
             } else {
-                if (W == 8) lpc_chunk<8, P_WIDE>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
-                else if (W == 16) lpc_chunk<16, P_WIDE>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
-                else lpc_chunk<32, P_WIDE>(row, c, hh, ht, n0, nvalid, h.order, h.shift, h.wasted);
+                if (h.type == T_FIXED || h.type == T_LPC || h.type == T_VERB) {
+                    const uint32_t i0 = (n0 < h.order) ? h.order - n0 : 0u;
+                    if (ablate & 8u) {
+                        for (uint32_t i = i0; i < nvalid; i++) row[i] = (int32_t)i;
+                    } else {
+                        for (uint32_t i = i0; i < nvalid; i++) row[i] = next_val(b, rs, limit, trunc);
+                    }
+                }
+                if (ablate & 4u) {
+                    /* restore skipped (timing ablation) */
+                } else if (h.type == T_CONST) {
+                    for (uint32_t i = 0; i < nvalid; i++) row[i] = (int32_t)((uint32_t)h.cval << h.wasted);
+                } else if (h.type == T_VERB) {
+                    for (uint32_t i = 0; i < nvalid; i++) row[i] = (int32_t)((uint32_t)row[i] << h.wasted);
+                } else if (h.type == T_FIXED) {
+                    fixed_chunk(row, hh, n0, nvalid, h.order, h.wasted);
+                } else {
+                    LPC_DISPATCH(lpc_chunk, W, row, c, hh, ht, n0, nvalid, h.order, sh, h.wasted);
+                }
             }
         }
         __syncthreads();
@@ -977,6 +1163,9 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
         }
         if (fi.status != BNF_ST_OK) f_bad[fl] = 1;
     }
+    /* the rows are free now: stage the slice-by-8 CRC tables there */
+    lds_u16 *T = (lds_u16 *)(lds_u32 *)lds;
+    for (uint32_t i = lane; i < 8u * 256u; i += DEC_LANES) T[i] = (&g_crc16_tab[0][0])[i];
     __syncthreads();
     /* CRC-16 over [frame_off, end): split across the frame's channel lanes, combined by
      * polynomial shifts (CRC is linear: crc(A|B) = crc(A)*x^(8|B|) + crc(B)). */
@@ -989,7 +1178,7 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
         const uint64_t per = (len + nl - 1) / nl;
         const uint64_t s0 = fi.frame_off + min(len, per * ch), s1 = fi.frame_off + min(len, per * (ch + 1));
         if (!(ablate & 1u)) {
-            part = crc16_range(words, nwords, s0, s1);
+            part = crc16_range((const uint8_t *)words, s0, s1, T);
             seg_end = s1;
             part = crc16_shift(part, fi.frame_off + len - seg_end);
         }
@@ -1064,22 +1253,26 @@ static uint32_t ablate_flags() {
 
 void bnf_set_ablate(uint32_t v) { g_ablate = v; }
 
-hipError_t bnf_launch_parse(const uint32_t *words, uint32_t nwords, uint64_t nbytes, const uint64_t *frame_offs,
-                            uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
-                            uint64_t base_sample, bnf_frame_info *info, hipStream_t s) {
-    if (!nframes) return hipSuccess;
-    hipLaunchKernelGGL(k_parse, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nwords, nbytes, frame_offs, nframes,
-                       sp, out_sample_in, base_sample, info, ablate_flags());
+/* words: 16-byte aligned; the allocation must cover round_up(nbytes, 16) bytes. */
+hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
+                            bnf_stream_params sp, const uint64_t *out_sample_in, uint64_t base_sample,
+                            bnf_frame_info *info, hipStream_t s) {
+    if (!nframes || !nbytes) return hipSuccess;
+    hipLaunchKernelGGL(k_parse, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
+                       out_sample_in, base_sample, info, ablate_flags());
     return hipGetLastError();
 }
 
-hipError_t bnf_launch_decode(const uint32_t *words, uint32_t nwords, uint64_t nbytes, uint32_t nframes,
-                             bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
-                             bnf_frame_info *info, hipStream_t s) {
-    if (!nframes) return hipSuccess;
+hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
+                             uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
+                             hipStream_t s) {
+    if (!nframes || !nbytes) return hipSuccess;
     const uint32_t fpb = DEC_LANES / chn_lanes;
-    hipLaunchKernelGGL(k_decode, dim3((nframes + fpb - 1) / fpb), dim3(DEC_LANES), 0, s, words, nwords, nbytes, nframes,
-                       sp, chn_lanes, fmt, out, out_bytes, info, ablate_flags());
+    const dim3 grid((nframes + fpb - 1) / fpb);
+    hipLaunchKernelGGL(k_decode<8>, grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
+                       out_bytes, info, ablate_flags());
+    hipLaunchKernelGGL(k_decode<32>, grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
+                       out_bytes, info, ablate_flags());
     return hipGetLastError();
 }
 

@@ -40,10 +40,10 @@ hipError_t bnf_launch_sync_scan(const uint8_t *d, uint64_t n, uint32_t *d_block_
                                 uint64_t *d_out, uint32_t cap, hipStream_t s);
 uint32_t bnf_scan_blocks(uint64_t n);
 void bnf_set_ablate(uint32_t v);
-hipError_t bnf_launch_parse(const uint32_t *words, uint32_t nwords, uint64_t nbytes, const uint64_t *frame_offs,
+hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs,
                             uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
                             uint64_t base_sample, bnf_frame_info *info, hipStream_t s);
-hipError_t bnf_launch_decode(const uint32_t *words, uint32_t nwords, uint64_t nbytes, uint32_t nframes,
+hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes,
                              bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
                              bnf_frame_info *info, hipStream_t s);
 }
@@ -173,7 +173,7 @@ extern "C" BNFLAC_API int bnflac_index_frames(bnflac_ctx *ctx, const uint8_t *d_
 static int check_args(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, const bnflac_stream_params *sp,
                       const char *who) {
     if (!ctx || !sp) return fail(std::string(who) + ": null argument");
-    if (((uintptr_t)d_bytes) & 3u) return fail(std::string(who) + ": d_bytes must be 4-byte aligned");
+    if (((uintptr_t)d_bytes) & 15u) return fail(std::string(who) + ": d_bytes must be 16-byte aligned");
     if (sp->channels < 1 || sp->channels > 8) return fail(std::string(who) + ": channels must be 1..8");
     if (nbytes >= (1ull << 34)) return fail(std::string(who) + ": buffer larger than 16 GiB");
     return 0;
@@ -186,7 +186,7 @@ extern "C" BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_
     if (check_args(ctx, d_bytes, nbytes, sp, "bnflac_parse_frames")) return -1;
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
-    hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, (uint32_t)((nbytes + 3) / 4), nbytes, d_frame_offsets,
+    hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, d_frame_offsets,
                                     nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info, (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_parse: ") + hipGetErrorString(e));
 }
@@ -198,7 +198,7 @@ extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d
     if (out_format < 0 || out_format > 3) return fail("bnflac_decode_parsed: bad out_format");
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
-    hipError_t e = bnf_launch_decode((const uint32_t *)d_bytes, (uint32_t)((nbytes + 3) / 4), nbytes, nframes, p,
+    hipError_t e = bnf_launch_decode((const uint32_t *)d_bytes, nbytes, nframes, p,
                                      lanes_for(sp->channels), out_format, d_out, out_bytes, (bnf_frame_info *)d_info,
                                      (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_decode: ") + hipGetErrorString(e));
@@ -602,8 +602,7 @@ bool decode_window(Dec *d, uint64_t base) {
             }
             const uint32_t pcm_ch = 8; /* planar slots sized for any channel count */
             if (!d->d_info.grow(sizeof(bnf_frame_info) * ncand)) goto oom;
-            const uint32_t nwords = (uint32_t)((n + 3) / 4);
-            if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, nwords, n, (const uint64_t *)d->d_cand.p, ncand, sp,
+            if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, n, (const uint64_t *)d->d_cand.p, ncand, sp,
                                  nullptr, 0, (bnf_frame_info *)d->d_info.p, d->stream) != hipSuccess)
                 goto hip_fail;
             if (hipMemcpyAsync(d->info.data(), d->d_info.p, sizeof(bnf_frame_info) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
@@ -619,7 +618,7 @@ bool decode_window(Dec *d, uint64_t base) {
                 goto hip_fail;
             bnf_stream_params spd = sp;
             spd.channels = pcm_ch;
-            if (bnf_launch_decode((const uint32_t *)d->d_bytes.p, nwords, n, ncand, spd, 8, BNF_OUT_PLANAR32,
+            if (bnf_launch_decode((const uint32_t *)d->d_bytes.p, n, ncand, spd, 8, BNF_OUT_PLANAR32,
                                   (uint8_t *)d->d_pcm.p, (uint64_t)std::max<uint64_t>(tot, 1) * pcm_ch * 4,
                                   (bnf_frame_info *)d->d_info.p, d->stream) != hipSuccess)
                 goto hip_fail;
