@@ -53,16 +53,18 @@ typedef __attribute__((address_space(1))) const void gvoid;
 #define RING_LANE_DW 256  /* dwords per slot row (64 lanes x 4) */
 #define RING_DW (RING * RING_LANE_DW)
 
-/* MSB-first bit stream.  Window hi:lo (big-endian words) with the cursor `off` bits
- * into hi; nx = word `wi` (the next to enter the window). */
+/* MSB-first bit stream.  Window hi:lo (big-endian words); the cursor is 32-s bits into
+ * hi (s in [0,31]; s == 0 means the cursor sits at the start of lo), so the next 32 bits
+ * are alignbit(hi, lo, s) for every cursor position.  nx = raw (little-endian) word wi,
+ * the next to enter the window; it is re-read from the ring on every advance. */
 struct BR {
     const uint32_t *__restrict__ w; /* stream words (16-byte aligned base) */
     uint32_t nw;                    /* words readable (allocation covers nblk*4) */
     uint32_t nblk;                  /* 16-byte blocks readable */
     lds_u32 *ring;                  /* slot 0 of lane 0 (wave-uniform) */
     lds_u32 *lring;                 /* this lane's slot-0 entry */
-    uint32_t wi, off, hi, lo, nx;
-    uint32_t vend, iend;            /* blocks < vend landed in the ring; < iend issued */
+    uint32_t wi, s, hi, lo, nx;
+    uint32_t vendw, iend;           /* words < vendw landed in the ring; blocks < iend issued */
 };
 
 DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, uint32_t lane) {
@@ -71,24 +73,26 @@ DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, u
     b.nw = b.nblk * 4u;
     b.ring = ring;
     b.lring = ring + lane * 4u;
-    b.wi = b.off = b.hi = b.lo = b.nx = 0;
-    b.vend = b.iend = 0;
+    b.wi = 2;
+    b.s = b.hi = b.lo = b.nx = 0;
+    b.vendw = b.iend = 0;
 }
 
 DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+/* single-wave workgroups: LDS exchange between lanes needs only the LDS queue drained
+ * (and the compiler kept from reordering); no s_barrier, no vmcnt drain of stores/DMA */
+DEV void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-DEV uint32_t br_word(const BR &b, uint32_t w) {
-    uint32_t v = b.lring[((w & 0x1cu) << 6) + (w & 3u)];
-    if ((w >> 2) >= b.vend) v = (w < b.nw) ? b.w[w] : 0u; /* not landed: read HBM directly */
-    return __builtin_bswap32(v);
-}
+DEV uint32_t gword(const BR &b, uint32_t w) { return (w < b.nw) ? b.w[w] : 0u; }
+DEV uint32_t ring_word(const BR &b, uint32_t w) { return b.lring[((w & 0x1cu) << 6) + (w & 3u)]; }
 
-/* Issue the blocks this lane will need next (exec-masked LDS-DMA per ring slot).
- * Everything issued earlier has landed once the wait returns. */
+/* Issue the blocks this lane will need next (exec-masked LDS-DMA per ring slot).  Blocks
+ * issued earlier have landed once the wait returns.  The block of word wi is kept: br_adv
+ * re-reads it. */
 DEV void br_refill(BR &b) {
     wait_vm();
-    b.vend = b.iend;
-    const uint32_t need = b.wi >> 2; /* br_adv re-reads word wi: keep its block */
+    b.vendw = b.iend * 4u;
+    const uint32_t need = b.wi >> 2;
     const uint32_t lo = max(b.iend, need), hi = need + RING;
 #pragma unroll
     for (int s = 0; s < RING; s++) {
@@ -102,41 +106,46 @@ DEV void br_refill(BR &b) {
     b.iend = hi;
 }
 
-/* Blocking seek: fill the ring from the block holding `bit`, then load the window. */
+/* Rare path: word wi is not in the landed part of the ring (a jump, or a lane that
+ * consumed more than the ring held): wait for what is in flight, refill if still short. */
+DEV void br_land(BR &b) {
+    wait_vm();
+    b.vendw = b.iend * 4u;
+    if (b.wi >= b.vendw) {
+        br_refill(b);
+        wait_vm();
+        b.vendw = b.iend * 4u;
+    }
+}
+
+/* Blocking seek (subframe starts, skips). */
 DEV void br_seek(BR &b, uint64_t bit) {
-    const uint32_t w = (uint32_t)(bit >> 5);
-    b.off = (uint32_t)(bit & 31u);
-    b.wi = w; /* refill starts at block w>>2 */
-    b.iend = b.vend = w >> 2;
+    b.s = (uint32_t)(0u - bit) & 31u;
+    const uint32_t hw = (uint32_t)((bit + b.s) >> 5) - 1u; /* word holding the cursor (-1 at bit 0) */
+    b.hi = __builtin_bswap32(gword(b, hw));
+    b.lo = __builtin_bswap32(gword(b, hw + 1u));
+    b.wi = hw + 2u;
+    b.iend = b.wi >> 2;
     br_refill(b);
     wait_vm();
-    b.vend = b.iend;
-    b.hi = br_word(b, w);
-    b.lo = br_word(b, w + 1u);
-    b.nx = br_word(b, w + 2u);
-    b.wi = w + 2u;
+    b.vendw = b.iend * 4u;
+    b.nx = ring_word(b, b.wi);
 }
 
-/* Non-blocking jump forward (skips); words not yet in the ring come from HBM. */
-DEV void br_jump(BR &b, uint64_t bit) {
-    const uint32_t w = (uint32_t)(bit >> 5);
-    b.off = (uint32_t)(bit & 31u);
-    b.hi = br_word(b, w);
-    b.lo = br_word(b, w + 1u);
-    b.nx = br_word(b, w + 2u);
-    b.wi = w + 2u;
-}
-
-DEV uint64_t br_pos(const BR &b) { return ((uint64_t)(b.wi - 2u) << 5) + b.off; }
-DEV uint32_t br_peek(const BR &b) { return __funnelshift_l(b.lo, b.hi, b.off); }
-DEV void br_adv(BR &b, uint32_t n) { /* n <= 32; branch-free */
-    const uint32_t o = b.off + n;
-    const bool c = o >= 32u;
+DEV uint64_t br_pos(const BR &b) { return ((uint64_t)(b.wi - 1u) << 5) - b.s; }
+DEV uint32_t br_peek(const BR &b) { return __builtin_amdgcn_alignbit(b.hi, b.lo, b.s); }
+DEV void br_adv(BR &b, uint32_t n) { /* n <= 32; branch-free except the rare landing check */
+    const int32_t t = (int32_t)b.s - (int32_t)n;
+    const bool c = t < 0;
+    b.s = (uint32_t)t & 31u;
     b.hi = c ? b.lo : b.hi;
-    b.lo = c ? b.nx : b.lo;
-    b.off = o & 31u;
+    b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
     b.wi += c ? 1u : 0u;
-    b.nx = br_word(b, b.wi);
+    if (__builtin_expect(__any(b.wi >= b.vendw), 0)) br_land(b);
+    /* issue the ring read after the window update, so the wait for the previous word
+     * (one codeword old) is not merged with a wait for this one */
+    __builtin_amdgcn_sched_barrier(0);
+    b.nx = ring_word(b, b.wi);
 }
 DEV uint32_t br_read(BR &b, uint32_t n) { /* 0..32 bits */
     uint32_t v = n ? (br_peek(b) >> ((32u - n) & 31u)) : 0u;
@@ -150,7 +159,7 @@ DEV int32_t br_read_s(BR &b, uint32_t n) {
 }
 DEV void br_skip(BR &b, uint64_t n) {
     if (n <= 32) br_adv(b, (uint32_t)n);
-    else br_jump(b, br_pos(b) + n);
+    else br_seek(b, br_pos(b) + n);
 }
 /* count zeros up to and including the terminating 1 (read_unary_unsigned @0x10001960) */
 DEV bool br_unary(BR &b, uint32_t &q, uint64_t limit) {
@@ -439,9 +448,9 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
                 if ((since++ & 31u) == 0 && !(ablate & 32u)) br_refill(b);
                 const uint32_t w = br_peek(b);
                 const uint32_t q = w ? (uint32_t)__builtin_clz(w) : 32u;
-                if (q + k1 <= 32u) {
-                    br_adv(b, q + k1);
-                } else {
+                const bool fast = q + k1 <= 32u;
+                br_adv(b, fast ? q + k1 : 0u);
+                if (!fast) {
                     uint32_t qq;
                     if (!br_unary(b, qq, limit)) return BNF_ST_TRUNC;
                     br_adv(b, k);
@@ -638,16 +647,16 @@ DEV void read_partition(BR &b, RS &s) {
  * 32-bit unsigned, zig-zag). */
 DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc) {
     const uint32_t w = br_peek(b);
-    uint32_t q = w ? (uint32_t)__builtin_clz(w) : 32u;
-    uint32_t lsb;
-    if (q + 1u + k <= 32u) {
-        lsb = __builtin_amdgcn_ubfe(w, 31u - q - k, k);
-        br_adv(b, q + 1u + k);
-    } else {
+    const uint32_t q0 = w ? (uint32_t)__builtin_clz(w) : 32u; /* v_ffbh + v_min */
+    const uint32_t len = q0 + 1u + k;
+    const bool fast = len <= 32u;
+    uint32_t u = (q0 << k) | __builtin_amdgcn_ubfe(w, 31u - q0 - k, k);
+    br_adv(b, fast ? len : 0u);
+    if (!fast) { /* long unary prefix: read_unary_unsigned, then the k low bits */
+        uint32_t q;
         if (!br_unary(b, q, limit)) trunc = 1;
-        lsb = br_read(b, k);
+        u = (q << k) | br_read(b, k);
     }
-    const uint32_t u = (q << k) | lsb;
     return (int32_t)((u >> 1) ^ (0u - (u & 1u)));
 }
 
@@ -1066,7 +1075,6 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
         const uint32_t n0 = kc * CHUNK;
         const uint32_t nvalid = (active && n0 < bs) ? min((uint32_t)CHUNK, bs - n0) : 0u;
         if (nvalid) {
-            if (h.type != T_CONST) br_refill(b);
             bool fast = fast_ok && nvalid == CHUNK && n0 >= h.order;
             if (fast && rs.left == 0) {
                 if (rs.pidx < rs.nparts) read_partition(b, rs);
@@ -1098,8 +1106,11 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
                     LPC_DISPATCH(lpc_chunk, W, row, c, hh, ht, n0, nvalid, h.order, sh, h.wasted);
                 }
             }
+            /* stage the next chunk's blocks now: the wait inside finds the previous DMAs
+             * and the previous chunk's PCM stores long done */
+            if (h.type != T_CONST && n0 + CHUNK < bs) br_refill(b);
         }
-        __syncthreads();
+        lds_sync();
         switch ((ablate & 2u) ? -1 : fmt) {
         case -1:
             break;
@@ -1117,7 +1128,7 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
                                            sp.bps == 24 ? 3u : 2u, out);
             break;
         }
-        __syncthreads();
+        lds_sync();
     }
 
     /* ---- last subframe end, zero padding, CRC-16 (read_frame_ @0x100118c0 tail) */

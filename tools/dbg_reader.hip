@@ -27,13 +27,13 @@ __global__ void __launch_bounds__(64) k_test(const uint32_t *words, uint64_t nby
         if ((mode == 0 || mode == 4) && (i & 7) == 0) br_refill(b);
         if (mode == 3 && (i & 7) == 0) {
             br_refill(b);
-            const uint32_t need = (b.wi + 1u) >> 2;
-            for (uint32_t j = need; j < b.vend; j++)
+            const uint32_t need = b.wi >> 2;
+            for (uint32_t j = need; j < b.vendw / 4; j++)
                 for (uint32_t q = 0; q < 4; q++) {
                     const uint32_t w = j * 4 + q;
                     const uint32_t g = b.lring[((w & 0x1cu) << 6) + (w & 3u)];
                     const uint32_t e = w < b.nw ? b.w[w] : 0u;
-                    if (g != e) { if (!rbad) { rinfo = (i << 16) | ((j - need) << 8) | (b.vend - need); rgot = g; rexp = e; } rbad++; }
+                    if (g != e) { if (!rbad) { rinfo = (i << 16) | ((j - need) << 8) | (b.vendw / 4 - need); rgot = g; rexp = e; } rbad++; }
                 }
         }
         if (mode == 1 && (i & 31) == 0 && lane < 32) br_refill(b);
@@ -41,8 +41,8 @@ __global__ void __launch_bounds__(64) k_test(const uint32_t *words, uint64_t nby
         if (br_pos(b) != pos) { bad++; if (first == 0xffffffffu) { first = i | 0x80000000u; } }
         const uint32_t v = br_read(b, n);
         if (mode == 4) {
-            const uint32_t e2 = b.wi < b.nw ? __builtin_bswap32(b.w[b.wi]) : 0u;
-            if (b.nx != e2 && !rbad) { rbad = 1; rinfo = i; rgot = b.wi - ((uint32_t)(pos >> 5)); rexp = (b.vend << 16) | (b.iend - (b.wi >> 2)); }
+            const uint32_t e2 = b.wi < b.nw ? b.w[b.wi] : 0u;
+            if (b.nx != e2 && !rbad) { rbad = 1; rinfo = i; rgot = b.wi - ((uint32_t)(pos >> 5)); rexp = (b.vendw << 16) | (b.iend - (b.wi >> 2)); }
         }
         const uint32_t e = ref_bits((const uint8_t *)words, nbytes, pos, n);
         if (v != e) { bad++; if (first == 0xffffffffu) { first = i; got0 = v; exp0 = e; } }
