@@ -45,6 +45,7 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
+    ap.add_argument("--stats", action="store_true", help="report k_decode event counters (one extra step)")
     ap.add_argument("--ablate", default=None,
                     help="comma list of ablation bitmasks to time after the measurement (timing only, wrong output): "
                          "1 CRC, 2 stores, 4 restore, 8 rice, 16 parse walk")
@@ -185,6 +186,17 @@ def main():
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(t_decode, 4),
                      "k_parse_avg_ms": round(t_parse, 4), "step_achieved_GBs": round(step_achieved, 1)},
     }
+    if args.stats and rank == 0:
+        import ctypes
+        buf = (ctypes.c_uint64 * 8)()
+        dec.L.bnflac_debug_stats(buf, 1)
+        dec.L.bnflac_debug_set_ablate(0x100)
+        step()
+        torch.cuda.synchronize(dev)
+        dec.L.bnflac_debug_stats(buf, 1)
+        dec.L.bnflac_debug_set_ablate(0)
+        names = ["fused_chunks", "generic_chunks", "dma_land_waits", "slow_rice", "refills", "waves"]
+        line["stats"] = {n: int(buf[i]) for i, n in enumerate(names)}
     if args.ablate and rank == 0:
         abl = []
         for m in [int(x, 0) for x in args.ablate.split(",")]:

@@ -43,15 +43,20 @@ __constant__ uint8_t g_crc8_tab[256];
 __constant__ uint16_t g_crc16_tab[8][256]; /* slice-by-8 */
 __constant__ uint16_t g_crc16_xpow[40];    /* x^(8*2^j) mod P for j < 40 */
 
+/* Debug event counters (wave-level events, enabled by ablate bit 0x100; timing runs
+ * leave them off).  0 fused chunks, 1 generic chunks, 2 DMA landing waits, 3 slow Rice
+ * codewords, 4 refills, 5 waves. */
+__device__ unsigned long long g_stats[8];
+#define STAT(on, i) do { if (on) { if (__builtin_amdgcn_read_exec() && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) atomicAdd(&g_stats[i], 1ull); } } while (0)
+
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void gvoid;
 
 /* ----------------------------------------------------------------- bit reader */
-#define RING 8            /* 16-byte slots per lane */
+#define RING_MAX 8        /* 16-byte slots per lane (k_parse; k_decode<8> uses 4) */
 #define RING_LANE_DW 256  /* dwords per slot row (64 lanes x 4) */
-#define RING_DW (RING * RING_LANE_DW)
 
 /* MSB-first bit stream.  Window hi:lo (big-endian words); the cursor is 32-s bits into
  * hi (s in [0,31]; s == 0 means the cursor sits at the start of lo), so the next 32 bits
@@ -62,20 +67,25 @@ struct BR {
     uint32_t nw;                    /* words readable (allocation covers nblk*4) */
     uint32_t nblk;                  /* 16-byte blocks readable */
     lds_u32 *ring;                  /* slot 0 of lane 0 (wave-uniform) */
-    lds_u32 *lring;                 /* this lane's slot-0 entry */
+    lds_u32 *lring;                 /* this lane's word-0 entry */
+    uint32_t rdepth, wmask;         /* ring slots (power of 2 <= RING_MAX); ring word mask */
     uint32_t wi, s, hi, lo, nx;
     uint32_t vendw, iend;           /* words < vendw landed in the ring; blocks < iend issued */
+    bool stats;
 };
 
-DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, uint32_t lane) {
+DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, uint32_t lane, uint32_t rdepth) {
+    b.rdepth = rdepth;
+    b.wmask = 4u * rdepth - 1u;
     b.w = words;
     b.nblk = (uint32_t)((nbytes + 15u) >> 4);
     b.nw = b.nblk * 4u;
     b.ring = ring;
-    b.lring = ring + lane * 4u;
+    b.lring = ring + lane;
     b.wi = 2;
     b.s = b.hi = b.lo = b.nx = 0;
     b.vendw = b.iend = 0;
+    b.stats = false;
 }
 
 DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -84,7 +94,8 @@ DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 DEV void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 DEV uint32_t gword(const BR &b, uint32_t w) { return (w < b.nw) ? b.w[w] : 0u; }
-DEV uint32_t ring_word(const BR &b, uint32_t w) { return b.lring[((w & 0x1cu) << 6) + (w & 3u)]; }
+/* ring layout [slot][word][lane]: a lane's read hits bank `lane`, conflict-free */
+DEV uint32_t ring_word(const BR &b, uint32_t w) { return b.lring[(w & b.wmask) << 6]; }
 
 /* Issue the blocks this lane will need next (exec-masked LDS-DMA per ring slot).  Blocks
  * issued earlier have landed once the wait returns.  The block of word wi is kept: br_adv
@@ -93,14 +104,16 @@ DEV void br_refill(BR &b) {
     wait_vm();
     b.vendw = b.iend * 4u;
     const uint32_t need = b.wi >> 2;
-    const uint32_t lo = max(b.iend, need), hi = need + RING;
+    const uint32_t lo = max(b.iend, need), hi = need + b.rdepth;
 #pragma unroll
-    for (int s = 0; s < RING; s++) {
-        const uint32_t j = lo + (((uint32_t)s - lo) & (RING - 1u));
+    for (int s = 0; s < RING_MAX; s++) {
+        if ((uint32_t)s >= b.rdepth) break; /* wave-uniform */
+        const uint32_t j = lo + (((uint32_t)s - lo) & (b.rdepth - 1u));
         if (j < hi) {
-            const uint32_t jj = min(j, b.nblk - 1u);
-            __builtin_amdgcn_global_load_lds((gvoid *)(b.w + (uint64_t)jj * 4u), (lds_void *)(b.ring + s * RING_LANE_DW),
-                                             16, 0, 0);
+            const uint32_t *src = b.w + (uint64_t)min(j, b.nblk - 1u) * 4u;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                __builtin_amdgcn_global_load_lds((gvoid *)(src + q), (lds_void *)(b.ring + (s * 4 + q) * 64), 4, 0, 0);
         }
     }
     b.iend = hi;
@@ -109,6 +122,7 @@ DEV void br_refill(BR &b) {
 /* Rare path: word wi is not in the landed part of the ring (a jump, or a lane that
  * consumed more than the ring held): wait for what is in flight, refill if still short. */
 DEV void br_land(BR &b) {
+    STAT(b.stats, 2);
     wait_vm();
     b.vendw = b.iend * 4u;
     if (b.wi >= b.vendw) {
@@ -360,7 +374,7 @@ struct SubHdr {
 /* read_subframe_ @0x10012480 up to (and including) the residual coding header.
  * warm/coef receive up to 32 values.  Returns BNF_ST_*; on ERROR sets err and the
  * reader position is where libFLAC stops. */
-template <bool STORE>
+template <bool STORE, int NW = 32>
 DEV uint32_t parse_subframe_head(BR &b, uint32_t bps, uint32_t bs, uint64_t limit, SubHdr &h,
                                  int32_t *warm, int32_t *coef, int32_t &err) {
     uint32_t x = br_read(b, 8);
@@ -400,7 +414,7 @@ DEV uint32_t parse_subframe_head(BR &b, uint32_t bps, uint32_t bs, uint64_t limi
     }
     for (uint32_t u = 0; u < h.order; u++) {
         int32_t v = br_read_s(b, bps);
-        if (STORE) warm[u] = v;
+        if (STORE && u < (uint32_t)NW) warm[u] = v;
     }
     if (h.type == T_LPC) {
         uint32_t p = br_read(b, 4);
@@ -409,7 +423,7 @@ DEV uint32_t parse_subframe_head(BR &b, uint32_t bps, uint32_t bs, uint64_t limi
         h.shift = br_read_s(b, 5);
         for (uint32_t u = 0; u < h.order; u++) {
             int32_t v = br_read_s(b, h.prec);
-            if (STORE) coef[u] = v;
+            if (STORE && u < (uint32_t)NW) coef[u] = v;
         }
         uint32_t ilog = 31u - (uint32_t)__builtin_clz(h.order);
         if (bps + h.prec + ilog <= 32) h.path = (bps <= 16 && h.prec <= 16 && h.order >= 4) ? P_MMX16 : P_IA32;
@@ -450,10 +464,12 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
                 const uint32_t q = w ? (uint32_t)__builtin_clz(w) : 32u;
                 const bool fast = q + k1 <= 32u;
                 br_adv(b, fast ? q + k1 : 0u);
-                if (!fast) {
-                    uint32_t qq;
-                    if (!br_unary(b, qq, limit)) return BNF_ST_TRUNC;
-                    br_adv(b, k);
+                if (__builtin_expect(__any(!fast), 0)) {
+                    if (!fast) {
+                        uint32_t qq;
+                        if (!br_unary(b, qq, limit)) return BNF_ST_TRUNC;
+                        br_adv(b, k);
+                    }
                 }
             }
         }
@@ -553,7 +569,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
                                               uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate) {
-    __shared__ uint32_t ring[RING_DW];
+    __shared__ uint32_t ring[RING_MAX * RING_LANE_DW];
     const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
     bnf_frame_info fi;
@@ -574,7 +590,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     const uint64_t limit = nbytes * 8u;
     const uint64_t fbit = fi.frame_off * 8u;
     BR b;
-    br_init(b, words, nbytes, (lds_u32 *)ring, threadIdx.x);
+    br_init(b, words, nbytes, (lds_u32 *)ring, threadIdx.x, RING_MAX);
     uint32_t st = parse_header(b, fbit, limit, sp, fi);
     if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
     if (st == BNF_ST_OK) {
@@ -621,8 +637,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
 
 /* ================================================================== k_decode */
 #define DEC_LANES 64
-#define CHUNK 32
-#define ROW (CHUNK + 1)
+#define RP 68 /* row-buffer stride (dwords) between samples: [sample][lane], 16-byte skew */
 
 struct RS { /* residual reader state */
     uint32_t verb;   /* 1: VERBATIM raw values of `k` bits */
@@ -652,10 +667,13 @@ DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc) {
     const bool fast = len <= 32u;
     uint32_t u = (q0 << k) | __builtin_amdgcn_ubfe(w, 31u - q0 - k, k);
     br_adv(b, fast ? len : 0u);
-    if (!fast) { /* long unary prefix: read_unary_unsigned, then the k low bits */
-        uint32_t q;
-        if (!br_unary(b, q, limit)) trunc = 1;
-        u = (q << k) | br_read(b, k);
+    if (__builtin_expect(__any(!fast), 0)) { /* wave-uniform test; the work is per lane */
+        STAT(b.stats, 3);
+        if (!fast) { /* long unary prefix: read_unary_unsigned, then the k low bits */
+            uint32_t q;
+            if (!br_unary(b, q, limit)) trunc = 1;
+            u = (q << k) | br_read(b, k);
+        }
     }
     return (int32_t)((u >> 1) ^ (0u - (u & 1u)));
 }
@@ -729,24 +747,24 @@ DEV void lpc_push(int32_t (&h)[N], int32_t (&ht)[4], int i, int32_t s) {
 
 /* Generic LPC restore of one chunk (rows hold residuals on entry, samples << wasted on
  * exit); handles warm-up samples and short chunks. */
-template <int W, int P, int N>
+template <int CH, int W, int P, int N>
 DEV void lpc_chunk(int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4], uint32_t n0,
                    uint32_t nvalid, uint32_t order, int32_t sh, uint32_t wasted) {
 #pragma unroll
-    for (int i = 0; i < CHUNK; i++) {
+    for (int i = 0; i < CH; i++) {
         const uint32_t n = n0 + (uint32_t)i;
         if ((uint32_t)i < nvalid) {
             int32_t s;
             if (n < order) {
                 s = h[i % W];
-                if (P == P_MMX16) s = row[i]; /* raw warm-up kept in the row */
+                if (P == P_MMX16) s = row[i * RP]; /* raw warm-up kept in the row */
             } else {
-                s = (int32_t)((uint32_t)row[i] + (uint32_t)lpc_pred<W, P>(c, h, ht, i, sh));
+                s = (int32_t)((uint32_t)row[i * RP] + (uint32_t)lpc_pred<W, P>(c, h, ht, i, sh));
                 if (P == P_MMX16) ht[i & 3] = tr16(s);
             }
             if (P == P_MMX16) h[i % W] = sat16(s);
             else h[i % W] = s;
-            row[i] = (int32_t)((uint32_t)s << wasted);
+            row[i * RP] = (int32_t)((uint32_t)s << wasted);
         }
     }
 }
@@ -754,17 +772,17 @@ DEV void lpc_chunk(int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t
 /* Fused Rice decode + LPC restore of a full chunk past the warm-up, inside one Rice
  * partition (parameter k, not escaped): the residual never leaves registers and the
  * two dependency chains (bit cursor, predictor) interleave. */
-template <int W, int P, int N>
+template <int CH, int W, int P, int N>
 DEV void lpc_fused(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
                    int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc) {
 #pragma unroll 1
-    for (int j = 0; j < CHUNK; j += W) {
+    for (int j = 0; j < CH; j += W) {
 #pragma unroll
         for (int t = 0; t < W; t++) {
             const int32_t r = rice_one(b, k, limit, trunc);
             const int32_t s = (int32_t)((uint32_t)r + (uint32_t)lpc_pred<W, P>(c, h, ht, t, sh));
             lpc_push<W, P>(h, ht, t, s);
-            row[j + t] = (int32_t)((uint32_t)s << wasted);
+            row[(j + t) * RP] = (int32_t)((uint32_t)s << wasted);
         }
     }
 }
@@ -783,31 +801,31 @@ DEV uint32_t fixed_pred(const int32_t (&h)[N], int i, uint32_t order) {
     }
 }
 
-template <int N>
+template <int CH, int N>
 DEV void fixed_chunk(int32_t *row, int32_t (&h)[N], uint32_t n0, uint32_t nvalid, uint32_t order, uint32_t wasted) {
 #pragma unroll
-    for (int i = 0; i < CHUNK; i++) {
+    for (int i = 0; i < CH; i++) {
         const uint32_t n = n0 + (uint32_t)i;
         if ((uint32_t)i < nvalid) {
             uint32_t s;
             if (n < order) s = (uint32_t)h[i & 7];
-            else s = (uint32_t)row[i] + fixed_pred(h, i, order);
+            else s = (uint32_t)row[i * RP] + fixed_pred(h, i, order);
             h[i & 7] = (int32_t)s;
-            row[i] = (int32_t)(s << wasted);
+            row[i * RP] = (int32_t)(s << wasted);
         }
     }
 }
 
-template <int N>
+template <int CH, int N>
 DEV void fixed_fused(BR &b, uint32_t k, int32_t *row, int32_t (&h)[N], uint32_t order, uint32_t wasted,
                      uint64_t limit, uint32_t &trunc) {
 #pragma unroll 1
-    for (int j = 0; j < CHUNK; j += 8) {
+    for (int j = 0; j < CH; j += 8) {
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const uint32_t s = (uint32_t)rice_one(b, k, limit, trunc) + fixed_pred(h, t, order);
             h[t] = (int32_t)s;
-            row[j + t] = (int32_t)(s << wasted);
+            row[(j + t) * RP] = (int32_t)(s << wasted);
         }
     }
 }
@@ -862,35 +880,69 @@ DEV uint32_t crc16_shift(uint32_t crc, uint64_t nbytes) {
     return crc;
 }
 
-template <int FMT>
-DEV void pack_chunk(const int32_t *lds, uint32_t lane, uint32_t fpb, uint32_t chn_lanes, uint32_t n0,
-                    const uint32_t *f_bs, const uint32_t *f_ch, const uint32_t *f_as, const uint64_t *f_out,
-                    const uint32_t *f_ok, uint32_t stream_channels, uint32_t fr_bytes, uint8_t *__restrict__ out) {
-    const uint32_t slots = fpb * CHUNK;
-    for (uint32_t slot = lane; slot < slots; slot += DEC_LANES) {
-        const uint32_t f = slot / CHUNK, i = slot % CHUNK;
-        const uint32_t n = n0 + i;
-        if (!f_ok[f] || n >= f_bs[f]) continue;
-        const int32_t *rows = lds + (f * chn_lanes) * ROW + i;
-        const uint32_t C = f_ch[f];
+/* Channel decorrelation (read_frame_ @0x10011a37-0x10011adb), 32-bit wrap. */
+DEV void decorrelate(uint32_t as, int32_t &v0, int32_t &v1) {
+    if (as == 1) v1 = (int32_t)((uint32_t)v0 - (uint32_t)v1);
+    else if (as == 2) v0 = (int32_t)((uint32_t)v0 + (uint32_t)v1);
+    else if (as == 3) {
+        uint32_t mid = (uint32_t)v0, side = (uint32_t)v1;
+        mid = (mid << 1) | (side & 1u);
+        v0 = (int32_t)(mid + side) >> 1;
+        v1 = (int32_t)(mid - side) >> 1;
+    }
+}
+
+/* Pack one chunk: every lane writes a contiguous run of CH/chn_lanes samples of its own
+ * frame (metadata in registers), reading the frame's channel rows from LDS.  Stereo
+ * FLACDecoder / interleaved-int32 runs go out as 16-byte stores. */
+template <int FMT, int CH>
+DEV void pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, uint32_t n0, bool fok, uint32_t bs,
+                   uint32_t C, uint32_t as, uint64_t os, uint32_t stream_channels, uint32_t fr_bytes,
+                   uint8_t *__restrict__ out) {
+    const uint32_t per = CH / chn_lanes;
+    const uint32_t fl = lane / chn_lanes, part = lane % chn_lanes;
+    const uint32_t i0 = part * per;
+    if (!fok || n0 + i0 >= bs) return;
+    const uint32_t cnt = min(per, bs - (n0 + i0));
+    const int32_t *rows = lds + i0 * RP + fl * chn_lanes; /* channel c of sample q: rows[q * RP + c] */
+    const uint64_t s0 = os + n0 + i0; /* first output sample of this run */
+    const uintptr_t dst = (uintptr_t)out + (uintptr_t)s0 * (FMT == BNF_OUT_INTERLEAVED32 ? 8u : 4u);
+    if ((FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_INTERLEAVED32) && C == 2 && chn_lanes == 2 && cnt == CH / 2 &&
+        (FMT == BNF_OUT_FLACDECODER || stream_channels == 2) && (dst & 15u) == 0) {
+        constexpr int PER = CH / 2;
+        int32_t l[PER], r[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const int2 v = *(const int2 *)(rows + q * RP); /* (L, R): lanes 2f, 2f+1 */
+            l[q] = v.x;
+            r[q] = v.y;
+        }
+#pragma unroll
+        for (int q = 0; q < PER; q++) decorrelate(as, l[q], r[q]);
+        if (FMT == BNF_OUT_FLACDECODER) { /* FLACDecoder.cs:543-562: L | R << 16 */
+            uint4 *o = (uint4 *)dst;
+#pragma unroll
+            for (int q = 0; q < PER; q += 4)
+                o[q / 4] = make_uint4(((uint32_t)l[q] & 0xffffu) | ((uint32_t)r[q] << 16),
+                                      ((uint32_t)l[q + 1] & 0xffffu) | ((uint32_t)r[q + 1] << 16),
+                                      ((uint32_t)l[q + 2] & 0xffffu) | ((uint32_t)r[q + 2] << 16),
+                                      ((uint32_t)l[q + 3] & 0xffffu) | ((uint32_t)r[q + 3] << 16));
+        } else {
+            int4 *o = (int4 *)dst;
+#pragma unroll
+            for (int q = 0; q < PER; q += 2) o[q / 2] = make_int4(l[q], r[q], l[q + 1], r[q + 1]);
+        }
+        return;
+    }
+    for (uint32_t q = 0; q < cnt; q++) {
+        const uint32_t n = n0 + i0 + q;
         int32_t v[8];
 #pragma unroll
-        for (int c = 0; c < 8; c++) v[c] = ((uint32_t)c < C) ? rows[c * ROW] : 0;
-        if (C == 2) { /* @0x10011a37-0x10011adb */
-            const uint32_t as = f_as[f];
-            if (as == 1) v[1] = (int32_t)((uint32_t)v[0] - (uint32_t)v[1]);
-            else if (as == 2) v[0] = (int32_t)((uint32_t)v[0] + (uint32_t)v[1]);
-            else if (as == 3) {
-                uint32_t mid = (uint32_t)v[0], side = (uint32_t)v[1];
-                mid = (mid << 1) | (side & 1u);
-                v[0] = (int32_t)(mid + side) >> 1;
-                v[1] = (int32_t)(mid - side) >> 1;
-            }
-        }
-        const uint64_t os = f_out[f];
+        for (int c = 0; c < 8; c++) v[c] = ((uint32_t)c < C) ? rows[q * RP + c] : 0;
+        if (C == 2) decorrelate(as, v[0], v[1]);
         if (FMT == BNF_OUT_PLANAR32) {
             int32_t *o = (int32_t *)out + os * stream_channels;
-            for (uint32_t c = 0; c < C; c++) o[(uint64_t)c * f_bs[f] + n] = v[c];
+            for (uint32_t c = 0; c < C; c++) o[(uint64_t)c * bs + n] = v[c];
         } else if (FMT == BNF_OUT_INTERLEAVED32) {
             int32_t *o = (int32_t *)out + (os + n) * stream_channels;
             for (uint32_t c = 0; c < C; c++) o[c] = v[c];
@@ -916,27 +968,28 @@ DEV void pack_chunk(const int32_t *lds, uint32_t lane, uint32_t fpb, uint32_t ch
 #define LPC_DISPATCH(FN, W_, ...)                                                                   \
     do {                                                                                             \
         if (h.path == P_MMX16) {                                                                     \
-            if (W_ == 8) FN<8, P_MMX16>(__VA_ARGS__);                                                \
-            else if (MAXW >= 16 && W_ == 16) FN<(MAXW >= 16 ? 16 : 8), P_MMX16>(__VA_ARGS__);        \
-            else if (MAXW >= 32) FN<(MAXW >= 32 ? 32 : 8), P_MMX16>(__VA_ARGS__);                    \
+            if (W_ == 8) FN<CHK, 8, P_MMX16>(__VA_ARGS__);                                                \
+            else if (MAXW >= 16 && W_ == 16) FN<CHK, (MAXW >= 16 ? 16 : 8), P_MMX16>(__VA_ARGS__);        \
+            else if (MAXW >= 32) FN<CHK, (MAXW >= 32 ? 32 : 8), P_MMX16>(__VA_ARGS__);                    \
         } else if (h.path == P_IA32) {                                                               \
-            if (W_ == 8) FN<8, P_IA32>(__VA_ARGS__);                                                 \
-            else if (MAXW >= 16 && W_ == 16) FN<(MAXW >= 16 ? 16 : 8), P_IA32>(__VA_ARGS__);         \
-            else if (MAXW >= 32) FN<(MAXW >= 32 ? 32 : 8), P_IA32>(__VA_ARGS__);                     \
+            if (W_ == 8) FN<CHK, 8, P_IA32>(__VA_ARGS__);                                                 \
+            else if (MAXW >= 16 && W_ == 16) FN<CHK, (MAXW >= 16 ? 16 : 8), P_IA32>(__VA_ARGS__);         \
+            else if (MAXW >= 32) FN<CHK, (MAXW >= 32 ? 32 : 8), P_IA32>(__VA_ARGS__);                     \
         } else {                                                                                     \
-            if (W_ == 8) FN<8, P_WIDE>(__VA_ARGS__);                                                 \
-            else if (MAXW >= 16 && W_ == 16) FN<(MAXW >= 16 ? 16 : 8), P_WIDE>(__VA_ARGS__);         \
-            else if (MAXW >= 32) FN<(MAXW >= 32 ? 32 : 8), P_WIDE>(__VA_ARGS__);                     \
+            if (W_ == 8) FN<CHK, 8, P_WIDE>(__VA_ARGS__);                                                 \
+            else if (MAXW >= 16 && W_ == 16) FN<CHK, (MAXW >= 16 ? 16 : 8), P_WIDE>(__VA_ARGS__);         \
+            else if (MAXW >= 32) FN<CHK, (MAXW >= 32 ? 32 : 8), P_WIDE>(__VA_ARGS__);                     \
         }                                                                                            \
     } while (0)
 
-template <int MAXW>
-__global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
+template <int MAXW, int CHK, int RD>
+__global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
                                                       uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                       int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
                                                       bnf_frame_info *__restrict__ info, uint32_t ablate) {
-    __shared__ uint32_t ring[RING_DW];
-    __shared__ int32_t lds[DEC_LANES * ROW];
+    static_assert(MAXW <= CHK && CHK % 8 == 0 && RD <= RING_MAX, "chunk must hold the predictor ring");
+    __shared__ uint32_t ring[RD * RING_LANE_DW];
+    __shared__ int32_t lds[CHK * RP]; /* [sample][lane] */
     __shared__ uint32_t f_bs[DEC_LANES], f_ch[DEC_LANES], f_as[DEC_LANES], f_ok[DEC_LANES];
     __shared__ uint64_t f_out[DEC_LANES];
     __shared__ uint32_t f_endbit[DEC_LANES], f_bad[DEC_LANES];
@@ -997,10 +1050,15 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
     __syncthreads();
     const bool fok = have && f_ok[fl];
     active = active && fok;
+    const uint32_t fbs = fok ? f_bs[fl] : 0u, fch = have ? fi.channels : 0u, fas = fok ? f_as[fl] : 0u;
+    const uint64_t fos = fok ? f_out[fl] : 0u;
+    const uint64_t f_off = have ? fi.frame_off : 0u;
 
     /* ---- subframe setup */
     BR b;
-    br_init(b, words, nbytes, (lds_u32 *)ring, lane);
+    br_init(b, words, nbytes, (lds_u32 *)ring, lane, RD);
+    b.stats = (ablate & 0x100u) != 0;
+    STAT(b.stats, 5);
     SubHdr h;
     h.type = T_CONST; h.order = 0; h.wasted = 0; h.bps = 0; h.shift = 0; h.path = P_IA32; h.cval = 0;
     h.porder = 0; h.rice2 = 0;
@@ -1017,12 +1075,12 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
     uint32_t bs = 0;
     int32_t sh = 0;
     bool fast_ok = false;
-    int32_t *row = lds + lane * ROW;
+    int32_t *row = lds + lane;
     if (active) {
         bs = fi.blocksize;
         br_seek(b, fi.frame_off * 8u + fi.sub_start[ch]);
-        int32_t warm[32], coef[32];
-        st = parse_subframe_head<true>(b, sub_bps(fi, ch), bs, limit, h, warm, coef, err);
+        int32_t warm[MAXW], coef[MAXW]; /* orders above MAXW are rejected below */
+        st = parse_subframe_head<true, MAXW>(b, sub_bps(fi, ch), bs, limit, h, warm, coef, err);
         if (st == BNF_ST_OK && h.type == T_LPC && h.order > MAXW) {
             st = BNF_ST_ERROR; /* k_parse mis-flagged: cannot happen for the subframes it read */
             err = E_UNPARSEABLE;
@@ -1054,11 +1112,13 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
             rs.psamples = h.porder ? bs >> h.porder : bs - h.order;
             rs.plen = h.rice2 ? 5u : 4u;
             rs.pesc = h.rice2 ? 31u : 15u;
-            fast_ok = (h.type == T_FIXED || h.type == T_LPC) && (h.porder == 0 || (rs.psamples % CHUNK) == 0) &&
-                      !(ablate & 12u);
+            /* fused path: partition boundaries on chunk boundaries; the k_decode<8> instance
+             * leaves 64-bit-accumulator subframes to the generic path (keeps it at 128 VGPRs) */
+            fast_ok = (h.type == T_FIXED || (h.type == T_LPC && (MAXW > 8 || h.path != P_WIDE))) &&
+                      (h.porder == 0 || (rs.psamples % CHK) == 0) && !(ablate & 12u);
             /* MMX path keeps raw warm-ups for output: stash them in the rows of chunk 0 */
             if (h.type == T_LPC && h.path == P_MMX16) {
-                for (uint32_t t = 0; t < h.order; t++) row[t] = warm[t];
+                for (uint32_t t = 0; t < h.order; t++) row[t * RP] = warm[t];
             }
         } else {
             active = false;
@@ -1068,111 +1128,121 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
     /* block-wide number of chunks */
     uint32_t mybs = active ? bs : 0u;
     for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
-    const uint32_t nchunks = (mybs + CHUNK - 1) / CHUNK;
+    const uint32_t nchunks = (mybs + CHK - 1) / CHK;
     const uint32_t W = h.order <= 8 ? 8u : (h.order <= 16 ? 16u : 32u);
 
     for (uint32_t kc = 0; kc < nchunks; kc++) {
-        const uint32_t n0 = kc * CHUNK;
-        const uint32_t nvalid = (active && n0 < bs) ? min((uint32_t)CHUNK, bs - n0) : 0u;
+        const uint32_t n0 = kc * CHK;
+        const uint32_t nvalid = (active && n0 < bs) ? min((uint32_t)CHK, bs - n0) : 0u;
         if (nvalid) {
-            bool fast = fast_ok && nvalid == CHUNK && n0 >= h.order;
+            bool fast = fast_ok && nvalid == CHK && n0 >= h.order;
             if (fast && rs.left == 0) {
                 if (rs.pidx < rs.nparts) read_partition(b, rs);
                 else fast = false;
             }
-            fast = fast && !rs.esc && rs.left >= CHUNK;
+            fast = fast && !rs.esc && rs.left >= CHK;
             if (fast) {
-                if (h.type == T_FIXED) fixed_fused(b, rs.k, row, hh, h.order, h.wasted, limit, trunc);
+                STAT(b.stats, 0);
+                if (h.type == T_FIXED) fixed_fused<CHK>(b, rs.k, row, hh, h.order, h.wasted, limit, trunc);
+                else if (MAXW == 8 && h.path == P_MMX16) lpc_fused<CHK, 8, P_MMX16>(b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
+                else if (MAXW == 8) lpc_fused<CHK, 8, P_IA32>(b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
                 else LPC_DISPATCH(lpc_fused, W, b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
-                rs.left -= CHUNK;
+                rs.left -= CHK;
             } else {
+                STAT(b.stats, 1);
                 if (h.type == T_FIXED || h.type == T_LPC || h.type == T_VERB) {
                     const uint32_t i0 = (n0 < h.order) ? h.order - n0 : 0u;
                     if (ablate & 8u) {
-                        for (uint32_t i = i0; i < nvalid; i++) row[i] = (int32_t)i;
+                        for (uint32_t i = i0; i < nvalid; i++) row[i * RP] = (int32_t)i;
                     } else {
-                        for (uint32_t i = i0; i < nvalid; i++) row[i] = next_val(b, rs, limit, trunc);
+                        for (uint32_t i = i0; i < nvalid; i++) row[i * RP] = next_val(b, rs, limit, trunc);
                     }
                 }
                 if (ablate & 4u) {
                     /* restore skipped (timing ablation) */
                 } else if (h.type == T_CONST) {
-                    for (uint32_t i = 0; i < nvalid; i++) row[i] = (int32_t)((uint32_t)h.cval << h.wasted);
+                    for (uint32_t i = 0; i < nvalid; i++) row[i * RP] = (int32_t)((uint32_t)h.cval << h.wasted);
                 } else if (h.type == T_VERB) {
-                    for (uint32_t i = 0; i < nvalid; i++) row[i] = (int32_t)((uint32_t)row[i] << h.wasted);
+                    for (uint32_t i = 0; i < nvalid; i++) row[i * RP] = (int32_t)((uint32_t)row[i * RP] << h.wasted);
                 } else if (h.type == T_FIXED) {
-                    fixed_chunk(row, hh, n0, nvalid, h.order, h.wasted);
+                    fixed_chunk<CHK>(row, hh, n0, nvalid, h.order, h.wasted);
                 } else {
                     LPC_DISPATCH(lpc_chunk, W, row, c, hh, ht, n0, nvalid, h.order, sh, h.wasted);
                 }
             }
             /* stage the next chunk's blocks now: the wait inside finds the previous DMAs
              * and the previous chunk's PCM stores long done */
-            if (h.type != T_CONST && n0 + CHUNK < bs) br_refill(b);
+            if (h.type != T_CONST && n0 + CHK < bs) {
+                STAT(b.stats, 4);
+                br_refill(b);
+            }
         }
         lds_sync();
         switch ((ablate & 2u) ? -1 : fmt) {
         case -1:
             break;
         case BNF_OUT_PLANAR32:
-            pack_chunk<BNF_OUT_PLANAR32>(lds, lane, fpb, chn_lanes, n0, f_bs, f_ch, f_as, f_out, f_ok, sp.channels, 0, out);
+            pack_lane<BNF_OUT_PLANAR32, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
             break;
         case BNF_OUT_INTERLEAVED32:
-            pack_chunk<BNF_OUT_INTERLEAVED32>(lds, lane, fpb, chn_lanes, n0, f_bs, f_ch, f_as, f_out, f_ok, sp.channels, 0, out);
+            pack_lane<BNF_OUT_INTERLEAVED32, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
             break;
         case BNF_OUT_FLACDECODER:
-            pack_chunk<BNF_OUT_FLACDECODER>(lds, lane, fpb, chn_lanes, n0, f_bs, f_ch, f_as, f_out, f_ok, sp.channels, 0, out);
+            pack_lane<BNF_OUT_FLACDECODER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
             break;
         default:
-            pack_chunk<BNF_OUT_FILEREADER>(lds, lane, fpb, chn_lanes, n0, f_bs, f_ch, f_as, f_out, f_ok, sp.channels,
-                                           sp.bps == 24 ? 3u : 2u, out);
+            pack_lane<BNF_OUT_FILEREADER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels,
+                                                     sp.bps == 24 ? 3u : 2u, out);
             break;
         }
         lds_sync();
     }
 
-    /* ---- last subframe end, zero padding, CRC-16 (read_frame_ @0x100118c0 tail) */
-    const bool last = fok && frame_ok && ch + 1 == fi.channels && fi.channels <= chn_lanes;
+    /* ---- last subframe end, zero padding, CRC-16 (read_frame_ @0x100118c0 tail).  The
+     * frame record is re-read here (only scalars stay live across the chunk loop). */
+    const bool last = fok && frame_ok && ch + 1 == fch && fch <= chn_lanes;
     if (active) {
         finish_partitions(b, rs);
         if (br_pos(b) > limit) trunc = 1;
     }
-    if (fok && frame_ok && ch < fi.channels && (st != BNF_ST_OK || trunc)) {
-        /* errors in a non-last subframe were already reported by k_parse; only the last
-         * subframe can fail here */
-        if (last) f_bad[fl] = 1;
-    }
+    uint32_t t_status = BNF_ST_OK, t_crc_read = 0;
+    int32_t t_err = -1;
+    uint64_t t_resume = 0;
+    bool t_resume_set = false;
     if (last) {
         if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
         if (st == BNF_ST_ERROR) {
-            fi.status = BNF_ST_ERROR;
-            fi.err = err;
-            fi.resume_bit = br_pos(b);
+            t_status = BNF_ST_ERROR;
+            t_err = err;
+            t_resume = br_pos(b);
+            t_resume_set = true;
         } else if (st == BNF_ST_TRUNC || trunc) {
-            fi.status = BNF_ST_TRUNC;
+            t_status = BNF_ST_TRUNC;
         } else {
             /* read_zero_padding_ @0x10012fe0 */
             const uint32_t padbits = (uint32_t)((8u - (br_pos(b) & 7u)) & 7u);
             const uint32_t z = br_read(b, padbits);
             if (br_pos(b) > limit) {
-                fi.status = BNF_ST_TRUNC;
+                t_status = BNF_ST_TRUNC;
             } else if (z != 0) {
-                fi.status = BNF_ST_ERROR;
-                fi.err = E_LOST_SYNC;
-                fi.resume_bit = br_pos(b);
+                t_status = BNF_ST_ERROR;
+                t_err = E_LOST_SYNC;
+                t_resume = br_pos(b);
+                t_resume_set = true;
             } else {
                 const uint64_t end_byte = br_pos(b) >> 3;
                 const uint32_t crc_read = br_read(b, 16);
                 if (br_pos(b) > limit) {
-                    fi.status = BNF_ST_TRUNC;
+                    t_status = BNF_ST_TRUNC;
                 } else {
-                    f_endbit[fl] = (uint32_t)(end_byte - fi.frame_off);
-                    fi.crc16_read = crc_read;
-                    fi.resume_bit = br_pos(b);
+                    f_endbit[fl] = (uint32_t)(end_byte - f_off);
+                    t_crc_read = crc_read;
+                    t_resume = br_pos(b);
+                    t_resume_set = true;
                 }
             }
         }
-        if (fi.status != BNF_ST_OK) f_bad[fl] = 1;
+        if (t_status != BNF_ST_OK) f_bad[fl] = 1;
     }
     /* the rows are free now: stage the slice-by-8 CRC tables there */
     lds_u16 *T = (lds_u16 *)(lds_u32 *)lds;
@@ -1181,30 +1251,33 @@ __global__ void __launch_bounds__(DEC_LANES) k_decode(const uint32_t *__restrict
     /* CRC-16 over [frame_off, end): split across the frame's channel lanes, combined by
      * polynomial shifts (CRC is linear: crc(A|B) = crc(A)*x^(8|B|) + crc(B)). */
     uint32_t part = 0;
-    uint64_t seg_end = 0;
-    const bool crc_lane = fok && frame_ok && ch < fi.channels && !f_bad[fl];
+    const bool crc_lane = fok && frame_ok && ch < fch && !f_bad[fl];
     if (crc_lane) {
         const uint64_t len = f_endbit[fl];
-        const uint32_t nl = fi.channels;
+        const uint32_t nl = fch;
         const uint64_t per = (len + nl - 1) / nl;
-        const uint64_t s0 = fi.frame_off + min(len, per * ch), s1 = fi.frame_off + min(len, per * (ch + 1));
+        const uint64_t s0 = f_off + min(len, per * ch), s1 = f_off + min(len, per * (ch + 1));
         if (!(ablate & 1u)) {
             part = crc16_range((const uint8_t *)words, s0, s1, T);
-            seg_end = s1;
-            part = crc16_shift(part, fi.frame_off + len - seg_end);
+            part = crc16_shift(part, f_off + len - s1);
         }
     }
     /* xor-reduce within each frame's lane group */
     uint32_t acc = part;
     for (uint32_t o = 1; o < chn_lanes; o <<= 1) acc ^= __shfl_xor(acc, o);
-    if ((ablate & 1u) && last && fi.status == BNF_ST_OK) acc = fi.crc16_read;
-    if (last && fi.status == BNF_ST_OK) {
-        fi.crc16_calc = acc;
-        fi.crc_ok = (acc == fi.crc16_read) ? 1u : 0u;
-        if (!fi.crc_ok) f_bad[fl] = 2; /* libFLAC zero-fills a CRC-failed frame (@0x10011af5) */
-        info[f] = fi;
-    } else if (last) {
-        info[f] = fi;
+    if ((ablate & 1u) && last && t_status == BNF_ST_OK) acc = t_crc_read;
+    if (last) {
+        bnf_frame_info fo = info[f];
+        fo.status = t_status;
+        if (t_status == BNF_ST_ERROR) fo.err = t_err;
+        if (t_resume_set) fo.resume_bit = t_resume;
+        if (t_status == BNF_ST_OK) {
+            fo.crc16_read = t_crc_read;
+            fo.crc16_calc = acc;
+            fo.crc_ok = (acc == t_crc_read) ? 1u : 0u;
+            if (!fo.crc_ok) f_bad[fl] = 2; /* libFLAC zero-fills a CRC-failed frame (@0x10011af5) */
+        }
+        info[f] = fo;
     }
     __syncthreads();
     /* zero-fill CRC-failed frames' output */
@@ -1264,6 +1337,15 @@ static uint32_t ablate_flags() {
 
 void bnf_set_ablate(uint32_t v) { g_ablate = v; }
 
+hipError_t bnf_stats(uint64_t *out8, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stats), 8 * sizeof(uint64_t));
+    if (e == hipSuccess && reset) {
+        static const uint64_t z[8] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z);
+    }
+    return e;
+}
+
 /* words: 16-byte aligned; the allocation must cover round_up(nbytes, 16) bytes. */
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
                             bnf_stream_params sp, const uint64_t *out_sample_in, uint64_t base_sample,
@@ -1280,9 +1362,9 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
     if (!nframes || !nbytes) return hipSuccess;
     const uint32_t fpb = DEC_LANES / chn_lanes;
     const dim3 grid((nframes + fpb - 1) / fpb);
-    hipLaunchKernelGGL(k_decode<8>, grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
+    hipLaunchKernelGGL((k_decode<8, 16, 4>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
                        out_bytes, info, ablate_flags());
-    hipLaunchKernelGGL(k_decode<32>, grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
+    hipLaunchKernelGGL((k_decode<32, 32, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
                        out_bytes, info, ablate_flags());
     return hipGetLastError();
 }

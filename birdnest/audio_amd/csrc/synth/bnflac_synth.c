@@ -383,6 +383,12 @@ static void encode_subframe(bw_t *w, const int32_t *x, unsigned bs, unsigned bps
     int32_t q[32];
     int shift;
     lpc_coefs(v, bs, ch.order, lp);
+    /* libFLAC 1.2.1's encoder keeps <= 17-bit subframes on the 32-bit restore path:
+     * qlp_coeff_precision = min(precision, 32 - subframe_bps - ilog2(order)) */
+    if (p->prec_clamp && sbps <= 17) {
+        const int lim = 32 - (int)sbps - (int)ilog2u(ch.order);
+        if (lim >= 1 && (int)ch.prec > lim) ch.prec = (unsigned)lim;
+    }
     quantize(lp, ch.order, ch.prec, q, &shift);
     int wide = (sbps + ch.prec + ilog2u(ch.order)) > 32;
     for (unsigned i = 0; i < ch.order; i++) bw_put_signed(w, v[i], (int)sbps);

@@ -59,6 +59,8 @@ typedef struct {
     int32_t write_header;       /* 1: "fLaC" + STREAMINFO (+ optional padding block) */
     int32_t force_sr_code;      /* -1 auto; else the 4-bit sample-rate code to use when valid */
     int32_t odd_headers;        /* 1: use 8/16-bit explicit blocksize and explicit-rate codes */
+    int32_t prec_clamp;         /* 1: clamp LPC precision like libFLAC's encoder (<= 17-bit subframes
+                                 * stay on the 32-bit restore path); 0: any precision (64-bit path) */
 } bnsyn_params;
 
 void bnsyn_default_params(bnsyn_params *p);

@@ -123,7 +123,7 @@ DECODER_SYMBOLS = [
 ]
 BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error", "bnflac_device_count",
                  "bnflac_index_frames", "bnflac_decode_frames", "bnflac_parse_frames", "bnflac_decode_parsed",
-                 "bnflac_out_stride", "bnflac_debug_set_ablate"]
+                 "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats"]
 
 _LIB = None
 
@@ -169,6 +169,8 @@ def load() -> ctypes.CDLL:
     L.bnflac_decode_parsed.restype = i
     L.bnflac_decode_parsed.argtypes = [p, p, ctypes.c_uint64, ctypes.c_uint32, p, i, p, ctypes.c_uint64, p, p]
     L.bnflac_debug_set_ablate.argtypes = [ctypes.c_uint32]
+    L.bnflac_debug_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.bnflac_debug_stats.restype = ctypes.c_int
     L.bnflac_out_stride.restype = ctypes.c_uint32
     L.bnflac_out_stride.argtypes = [i, p]
     _LIB = L

@@ -30,6 +30,7 @@ class _Params(ctypes.Structure):
         ("noise", ctypes.c_double), ("seed", ctypes.c_uint64), ("rice2", ctypes.c_int32),
         ("escape_permille", ctypes.c_int32), ("write_header", ctypes.c_int32),
         ("force_sr_code", ctypes.c_int32), ("odd_headers", ctypes.c_int32),
+        ("prec_clamp", ctypes.c_int32),
     ]
 
 
@@ -58,6 +59,7 @@ class SynthParams:
     write_header: int = 1
     force_sr_code: int = -1
     odd_headers: int = 0
+    prec_clamp: int = 0   # 1: libFLAC encoder's precision clamp (see bnflac_synth.c)
 
 
 @dataclasses.dataclass
@@ -77,9 +79,11 @@ CONFIGS = {
     # C1: 44.1k/16/2ch, 10 s, bs 4096 (107 x 4096 + 2728), FIXED-2
     "C1": SynthParams(nframes=108, blocksize=4096, last_blocksize=441000 - 107 * 4096,
                       subframe_mode=SUB_FIXED, order=2, partition_order=-1, stereo_mode=ST_CYCLE, seed=1),
-    # C2: 1024 frames x bs 4096, 44.1k/16/2ch, LPC-8, Rice partition order 4
+    # C2: 1024 frames x bs 4096, 44.1k/16/2ch, LPC-8, Rice partition order 4.  LPC precision
+    # clamped the way libFLAC 1.2.1's encoder does for 16-bit input, so subframes use the
+    # 32-bit restore paths as in real files; the unclamped 64-bit path is covered by tests.
     "C2": SynthParams(nframes=1024, blocksize=4096, subframe_mode=SUB_LPC, order=8,
-                      partition_order=4, stereo_mode=ST_INDEP, seed=2),
+                      partition_order=4, stereo_mode=ST_INDEP, seed=2, prec_clamp=1),
     # C3: 96k/24/2ch, LPC-12, bs 8192, wasted bits + mid/side (1024 frames)
     "C3": SynthParams(sample_rate=96000, bps=24, nframes=1024, blocksize=8192, subframe_mode=SUB_LPC,
                       order=12, partition_order=-1, stereo_mode=ST_MID_SIDE, wasted_bits_max=4,

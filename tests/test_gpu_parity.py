@@ -119,6 +119,27 @@ def test_config_batch_vs_oracle_and_source(gpu, cfg):
     assert np.array_equal(pcm, oracle.interleave(ev, opcm))
 
 
+@pytest.mark.parametrize("order,prec,stereo", [(2, 15, 0), (3, 0, 3), (4, 12, 0), (8, 15, 1), (8, 0, 2),
+                                                (12, 15, 3), (16, 0, 0), (32, 15, 3), (32, 0, 0)])
+def test_lpc_restore_paths_16bit(gpu, order, prec, stereo):
+    """Every libFLAC restore path on 16-bit input (MMX for order >= 4 at <= 32 bits, ia32
+    for low orders, the 64-bit path when bps + precision + log2(order) > 32 -- no encoder
+    precision clamp here), in both k_decode instances (orders <= 8 and above)."""
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    p = synth.config("C2", nframes=10, order=order, qlp_precision=prec, stereo_mode=stereo, prec_clamp=0,
+                     partition_order=-1 if order > 16 else 4, seed=100 + order)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    out, info, sp = _decode_batch(gpu, data, s.frame_offsets, libflac.OUT_INTERLEAVED32)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    pcm = out.view("<i4").reshape(-1, 2)
+    assert np.array_equal(pcm, s.pcm)
+    ev, opcm = oracle.run(data)
+    assert np.array_equal(pcm, oracle.interleave(ev, opcm))
+
+
 def test_flacdecoder_format_vs_oracle(gpu):
     import oracle
     from birdnest.audio_amd import synth

@@ -15,10 +15,10 @@ DEV uint32_t ref_bits(const uint8_t *d, uint64_t nbytes, uint64_t pos, uint32_t 
 }
 
 __global__ void __launch_bounds__(64) k_test(const uint32_t *words, uint64_t nbytes, uint32_t *res, int mode) {
-    __shared__ uint32_t ring[RING_DW];
+    __shared__ uint32_t ring[RING_MAX * RING_LANE_DW];
     BR b;
     const uint32_t lane = threadIdx.x;
-    br_init(b, words, nbytes, (lds_u32 *)ring, lane);
+    br_init(b, words, nbytes, (lds_u32 *)ring, lane, RING_MAX);
     uint64_t pos = (uint64_t)lane * 4099u + 5u + blockIdx.x * 100003u;
     br_seek(b, pos);
     uint32_t bad = 0, first = 0xffffffffu, got0 = 0, exp0 = 0;
@@ -31,7 +31,7 @@ __global__ void __launch_bounds__(64) k_test(const uint32_t *words, uint64_t nby
             for (uint32_t j = need; j < b.vendw / 4; j++)
                 for (uint32_t q = 0; q < 4; q++) {
                     const uint32_t w = j * 4 + q;
-                    const uint32_t g = b.lring[((w & 0x1cu) << 6) + (w & 3u)];
+                    const uint32_t g = ring_word(b, w);
                     const uint32_t e = w < b.nw ? b.w[w] : 0u;
                     if (g != e) { if (!rbad) { rinfo = (i << 16) | ((j - need) << 8) | (b.vendw / 4 - need); rgot = g; rexp = e; } rbad++; }
                 }
