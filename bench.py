@@ -44,6 +44,9 @@ def parse_args():
     ap.add_argument("--frames", type=int, default=1024, help="frames per batch (BASELINE C2: 1024)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads for the multi-thread CPU baseline (0: min(16, cpu count))")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-resident) measurement")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--stats", action="store_true", help="report k_decode event counters (one extra step)")
     ap.add_argument("--ablate", default=None,
@@ -52,21 +55,79 @@ def parse_args():
     return ap.parse_args()
 
 
-def cpu_baseline(data: bytes, nsamples_per_pass: int, budget_s: float):
-    """Oracle (restated libFLAC 1.2.1 + FLACDecoder.CopyTo pack), single thread."""
+def cpu_baseline(data: bytes, nsamples_per_pass: int, budget_s: float, threads: int = 1):
+    """Oracle (restated libFLAC 1.2.1 + FLACDecoder.CopyTo pack) on `threads` host threads,
+    each decoding whole batches independently (a libFLAC decoder is single-threaded per
+    stream; ctypes releases the GIL during the call)."""
+    import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.lib()
+    counts = [0] * threads
     t0 = time.perf_counter()
-    passes = 0
-    while True:
-        rc, pk, msg, _ = oracle.flacdecoder_copyto(data)
-        assert rc == 0, msg
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
+
+    def run(i):
+        while time.perf_counter() - t0 < budget_s:
+            rc, pk, msg, _ = oracle.flacdecoder_copyto(data)
+            assert rc == 0, msg
+            counts[i] += 1
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    passes = sum(counts)
     return passes * nsamples_per_pass / el / 1e6, passes, el
+
+
+def cpu_model() -> str:
+    try:
+        for l in open("/proc/cpuinfo"):
+            if l.startswith("model name"):
+                return l.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pcie_inclusive(args, torch, dev, libflac, dec, data, offs, sp, p, s, pcm_bytes, samples_per_batch, nb=8, reps=3):
+    """Host-resident caller: pinned host compressed bytes -> H2D -> parse+decode -> D2H PCM.
+    Reported beside `value`, never as it."""
+    copy_len = (len(data) + 255) // 256 * 256
+    h_in = torch.zeros(copy_len * nb + 64, dtype=torch.uint8).pin_memory()
+    src = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy())
+    for b in range(nb):
+        h_in[b * copy_len: b * copy_len + len(data)] = src
+    h_out = torch.empty(pcm_bytes * nb, dtype=torch.uint8).pin_memory()
+    d_in = torch.empty_like(h_in, device=dev)
+    d_out = torch.empty(pcm_bytes * nb, dtype=torch.uint8, device=dev)
+    d_offs = torch.from_numpy(np.concatenate([offs + b * copy_len for b in range(nb)])).to(dev)
+    fr_bs = np.full(args.frames, p.blocksize, dtype=np.int64)
+    fr_start = np.concatenate([[0], np.cumsum(fr_bs)[:-1]])
+    d_os = torch.from_numpy(np.concatenate([fr_start + b * int(s.nsamples) for b in range(nb)])).to(dev)
+    nf = args.frames * nb
+    d_info = torch.zeros(nf * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def once():
+        d_in.copy_(h_in, non_blocking=True)
+        dec.decode_frames(d_in, copy_len * nb, d_offs, nf, sp, libflac.OUT_FLACDECODER, d_out, d_info,
+                          d_out_sample=d_os, stream=stream)
+        h_out.copy_(d_out, non_blocking=True)
+
+    once()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    ok = h_out[:pcm_bytes].numpy().tobytes() == s.pcm.astype("<i2").tobytes()
+    return {"value": round(samples_per_batch * nb * reps / el / 1e6, 2), "unit": "MSamples/s",
+            "batches": nb * reps, "bitexact": bool(ok),
+            "note": "pinned host bytes -> H2D -> k_parse+k_decode -> D2H PCM, serialized on one stream"}
 
 
 def main():
@@ -211,12 +272,21 @@ def main():
                         "k_decode_ms": round(sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps, 4)})
         dec.L.bnflac_debug_set_ablate(0)
         line["ablation"] = abl
+    if rank == 0 and not args.no_pcie:
+        line["pcie_inclusive"] = pcie_inclusive(args, torch, dev, libflac, dec, data, offs, sp, p, s,
+                                                pcm_bytes_per_batch, samples_per_batch)
     if rank == 0 and not args.no_cpu_baseline:
         sys.stdout.flush()
-        mss, passes, el = cpu_baseline(data, samples_per_batch, args.cpu_seconds)
-        line["cpu_baseline"] = {"value": round(mss, 3), "unit": "MSamples/s", "cores": 1, "kind": "port",
+        nthr = args.cpu_threads or min(16, os.cpu_count() or 1)
+        mss1, passes1, el1 = cpu_baseline(data, samples_per_batch, args.cpu_seconds / 2, 1)
+        mss, passes, el = cpu_baseline(data, samples_per_batch, args.cpu_seconds / 2, nthr)
+        line["cpu_baseline"] = {"value": round(mss, 3), "unit": "MSamples/s", "cores": nthr, "kind": "port",
                                 "sample": f"{passes} x one C2 batch ({args.frames} frames, {samples_per_batch} samples) "
-                                          f"through the oracle's FLACDecoder.CopyTo replay, {el:.1f} s"}
+                                          f"through the oracle's FLACDecoder.CopyTo replay on {nthr} threads, "
+                                          f"{el:.1f} s",
+                                "single_thread": {"value": round(mss1, 3), "cores": 1, "passes": passes1,
+                                                  "seconds": round(el1, 2)},
+                                "cpu": cpu_model()}
     if rank == 0:
         js = json.dumps(line)
         print(js, flush=True)

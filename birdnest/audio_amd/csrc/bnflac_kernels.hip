@@ -89,6 +89,9 @@ DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, u
 }
 
 DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+/* vmcnt retires in issue order (loads, stores and LDS-DMA together): waiting until at most
+ * N are outstanding completes everything older than the youngest N */
+template <int N> DEV void wait_vm_but() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
 /* single-wave workgroups: LDS exchange between lanes needs only the LDS queue drained
  * (and the compiler kept from reordering); no s_barrier, no vmcnt drain of stores/DMA */
 DEV void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -100,8 +103,9 @@ DEV uint32_t ring_word(const BR &b, uint32_t w) { return b.lring[(w & b.wmask) <
 /* Issue the blocks this lane will need next (exec-masked LDS-DMA per ring slot).  Blocks
  * issued earlier have landed once the wait returns.  The block of word wi is kept: br_adv
  * re-reads it. */
+template <int KEEP = 0> /* KEEP: younger vector-memory ops (PCM stores) that may stay in flight */
 DEV void br_refill(BR &b) {
-    wait_vm();
+    wait_vm_but<KEEP>();
     b.vendw = b.iend * 4u;
     const uint32_t need = b.wi >> 2;
     const uint32_t lo = max(b.iend, need), hi = need + b.rdepth;
@@ -1174,7 +1178,9 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
              * and the previous chunk's PCM stores long done */
             if (h.type != T_CONST && n0 + CHK < bs) {
                 STAT(b.stats, 4);
-                br_refill(b);
+                /* since the previous refill this wave issued only the last pack's stores
+                 * (CHK/8 16-byte stores on the stereo path): let those drain in the background */
+                br_refill<CHK / 8>(b);
             }
         }
         lds_sync();

@@ -1,0 +1,84 @@
+"""N>1 path on CPU: contiguous frame sharding + gather of PCM to rank 0 (world size 2, gloo).
+
+The device decode is stood in for by the oracle here (test infrastructure, no GPU): each
+rank decodes only its own frame range, rank 0 gathers the packed PCM and checks it against
+a whole-stream decode -- the property bench.py's multi-GPU path relies on.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from birdnest.audio_amd import shard
+
+
+def test_partition_balanced_and_complete():
+    spf = [4096] * 100 + [192] * 50 + [16384] * 10
+    for world in (1, 2, 3, 8):
+        parts = shard.partition(spf, world)
+        assert parts[0][0] == 0 and parts[-1][1] == len(spf)
+        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+        loads = [sum(spf[s:e]) for s, e in parts]
+        assert max(loads) - min(loads) <= max(spf) * 2
+    assert shard.partition([], 4) == [(0, 0)] * 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _frame_pcm(oracle, data, off):
+    """Interleaved int32 [bs, ch] of the frame at byte `off` (oracle, planar -> interleaved)."""
+    rc, res, planar = oracle.decode_frame_at(data, off, None)
+    assert rc == 0 and res.error < 0 and res.crc_ok == 1
+    bs, ch = int(res.blocksize), int(res.channels)
+    return planar[: bs * ch].reshape(ch, bs).T.reshape(-1)
+
+
+def _worker(rank, world, port, data, offsets, blocksizes, result_q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import torch
+    import torch.distributed as dist
+    import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        start, end = shard.partition(blocksizes, world)[rank]
+        pcm = []
+        for f in range(start, end):
+            pcm.append(_frame_pcm(oracle, data, int(offsets[f])))
+        local = np.concatenate(pcm).astype("<i2").view(np.uint8) if pcm else np.zeros(0, np.uint8)
+        got = shard.gather_bytes(torch.from_numpy(local.copy()))
+        if rank == 0:
+            result_q.put(got.numpy().tobytes())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gather_matches_whole_stream():
+    import torch.multiprocessing as mp
+    from birdnest.audio_amd import synth
+    import oracle
+    p = synth.config("C4", nframes=24, seed=11)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    offs = [int(o) for o in s.frame_offsets]
+    bss = [len(_frame_pcm(oracle, data, o)) // p.channels for o in offs]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, data, offs, bss, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=120)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert got == s.pcm.astype("<i2").tobytes()
