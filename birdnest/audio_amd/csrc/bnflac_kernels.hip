@@ -46,7 +46,20 @@ __constant__ uint16_t g_crc16_xpow[40];    /* x^(8*2^j) mod P for j < 40 */
 /* Debug event counters (wave-level events, enabled by ablate bit 0x100; timing runs
  * leave them off).  0 fused chunks, 1 generic chunks, 2 DMA landing waits, 3 slow Rice
  * codewords, 4 refills, 5 waves. */
-__device__ unsigned long long g_stats[8];
+__device__ unsigned long long g_stats[16]; /* 8.. : s_memtime cycles per phase, summed over waves */
+/* Phase timers (s_memtime) for the debug counters; compiled in only with
+ * -DBNFLAC_PHASE_TIMERS, because a scalar-memory op anywhere in the loop makes hipcc's
+ * LDS waits conservative (lgkmcnt(0)). */
+DEV uint64_t tnow(bool on) { /* call at wave-uniform points only */
+#ifndef BNFLAC_PHASE_TIMERS
+    (void)on;
+    return 0ull;
+#endif
+    if (!on) return 0ull;
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return t;
+}
 #define STAT(on, i) do { if (on) { if (__builtin_amdgcn_read_exec() && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) atomicAdd(&g_stats[i], 1ull); } } while (0)
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -71,6 +84,7 @@ struct BR {
     uint32_t rdepth, wmask;         /* ring slots (power of 2 <= RING_MAX); ring word mask */
     uint32_t wi, s, hi, lo, nx;
     uint32_t vendw, iend;           /* words < vendw landed in the ring; blocks < iend issued */
+    uint32_t iend_old;              /* k_decode's 2-deep DMA pipeline: issued two refills ago */
     bool stats;
 };
 
@@ -81,10 +95,11 @@ DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, u
     b.nblk = (uint32_t)((nbytes + 15u) >> 4);
     b.nw = b.nblk * 4u;
     b.ring = ring;
-    b.lring = ring + lane;
+    b.lring = ring + lane * 4u;
     b.wi = 2;
     b.s = b.hi = b.lo = b.nx = 0;
     b.vendw = b.iend = 0;
+    b.iend_old = 0;
     b.stats = false;
 }
 
@@ -92,13 +107,32 @@ DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 /* vmcnt retires in issue order (loads, stores and LDS-DMA together): waiting until at most
  * N are outstanding completes everything older than the youngest N */
 template <int N> DEV void wait_vm_but() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+/* the same with a wave-uniform run-time count (vmcnt is an immediate: jump table) */
+DEV void wait_vm_n(uint32_t n) {
+    switch (__builtin_amdgcn_readfirstlane(min(n, 63u))) {
+#define WVN(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+#define WVN8(k) WVN(k) WVN(k + 1) WVN(k + 2) WVN(k + 3) WVN(k + 4) WVN(k + 5) WVN(k + 6) WVN(k + 7)
+        WVN8(0) WVN8(8) WVN8(16) WVN8(24) WVN8(32) WVN8(40) WVN8(48) WVN8(56)
+#undef WVN8
+#undef WVN
+    default: break;
+    }
+}
 /* single-wave workgroups: LDS exchange between lanes needs only the LDS queue drained
  * (and the compiler kept from reordering); no s_barrier, no vmcnt drain of stores/DMA */
 DEV void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 DEV uint32_t gword(const BR &b, uint32_t w) { return (w < b.nw) ? b.w[w] : 0u; }
-/* ring layout [slot][word][lane]: a lane's read hits bank `lane`, conflict-free */
-DEV uint32_t ring_word(const BR &b, uint32_t w) { return b.lring[(w & b.wmask) << 6]; }
+/* ring layout [slot][lane][4 words] (16 bytes per lane per slot, the LDS-DMA dwordx4
+ * image); block j lives in slot j % rdepth */
+DEV uint32_t ring_word(const BR &b, uint32_t w) {
+    const uint32_t t = w & b.wmask;
+    return b.lring[((t & ~3u) << 6) | (t & 3u)];
+}
+DEV void dma_block(const BR &b, uint32_t j, uint32_t slot) { /* one 16-byte block per lane */
+    __builtin_amdgcn_global_load_lds((gvoid *)(b.w + (uint64_t)min(j, b.nblk - 1u) * 4u),
+                                     (lds_void *)(b.ring + slot * RING_LANE_DW), 16, 0, 0);
+}
 
 /* Issue the blocks this lane will need next (exec-masked LDS-DMA per ring slot).  Blocks
  * issued earlier have landed once the wait returns.  The block of word wi is kept: br_adv
@@ -107,32 +141,32 @@ template <int KEEP = 0> /* KEEP: younger vector-memory ops (PCM stores) that may
 DEV void br_refill(BR &b) {
     wait_vm_but<KEEP>();
     b.vendw = b.iend * 4u;
-    const uint32_t need = b.wi >> 2;
+    /* whole 64-byte lines: [iend, first line of the cursor + rdepth) */
+    const uint32_t need = (b.wi >> 2) & ~3u;
     const uint32_t lo = max(b.iend, need), hi = need + b.rdepth;
 #pragma unroll
     for (int s = 0; s < RING_MAX; s++) {
         if ((uint32_t)s >= b.rdepth) break; /* wave-uniform */
         const uint32_t j = lo + (((uint32_t)s - lo) & (b.rdepth - 1u));
-        if (j < hi) {
-            const uint32_t *src = b.w + (uint64_t)min(j, b.nblk - 1u) * 4u;
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                __builtin_amdgcn_global_load_lds((gvoid *)(src + q), (lds_void *)(b.ring + (s * 4 + q) * 64), 4, 0, 0);
-        }
+        if (j < hi) dma_block(b, j, (uint32_t)s);
     }
-    b.iend = hi;
+    b.iend = max(b.iend, hi);
 }
 
 /* Rare path: word wi is not in the landed part of the ring (a jump, or a lane that
  * consumed more than the ring held): wait for what is in flight, refill if still short. */
+DEV void br_drained(BR &b) { /* every vector-memory op of this wave has completed (per lane) */
+    b.vendw = b.iend * 4u;
+    b.iend_old = b.iend;
+}
 DEV void br_land(BR &b) {
     STAT(b.stats, 2);
     wait_vm();
-    b.vendw = b.iend * 4u;
+    br_drained(b);
     if (b.wi >= b.vendw) {
         br_refill(b);
         wait_vm();
-        b.vendw = b.iend * 4u;
+        br_drained(b);
     }
 }
 
@@ -143,27 +177,82 @@ DEV void br_seek(BR &b, uint64_t bit) {
     b.hi = __builtin_bswap32(gword(b, hw));
     b.lo = __builtin_bswap32(gword(b, hw + 1u));
     b.wi = hw + 2u;
-    b.iend = b.wi >> 2;
+    b.iend = (b.wi >> 2) & ~3u;
     br_refill(b);
     wait_vm();
-    b.vendw = b.iend * 4u;
+    br_drained(b);
     b.nx = ring_word(b, b.wi);
+}
+
+/* k_decode's refill: a 2-deep pipeline.  Waits only for the DMAs issued two refills ago
+ * (vmcnt counts loads, stores and LDS-DMA together and retires them in issue order, so
+ * letting the younger q.s_last + q.d_last + q.s_prev ops stay outstanding is exact), marks
+ * those blocks landed, and issues the next blocks.  Blocks issued now become readable two
+ * chunks later; the ring keeps ~6 blocks ahead of the cursor.  Called by the whole wave
+ * (the counts must be wave-uniform); `want` masks the lanes that refill.  A full drain in
+ * between (br_land, seek) only completes more, so the counts stay safe without reset. */
+struct VmQ {
+    uint32_t d_last, s_last, s_prev; /* DMAs of the last refill; stores since it; before it */
+};
+DEV void br_refill2(BR &b, bool want, VmQ &q, bool nowait = false) {
+    if (!nowait) wait_vm_n(q.s_last + q.d_last + q.s_prev); /* nowait: timing ablation 0x200 only */
+    if (want) b.vendw = b.iend_old * 4u;
+    /* the ring holds rdepth/4 whole lines; a lane whose cursor (word wi) is in the newest
+     * line fetches the next line into the oldest line's slots: 4 x 16-byte DMAs hitting
+     * one cache line */
+    const uint32_t curl = (b.wi >> 2) & ~3u;
+    const bool go = want && b.iend <= curl + 4u;
+    const uint32_t slot0 = b.iend & (b.rdepth - 1u); /* multiple of 4 */
+    uint32_t d = 0;
+#pragma unroll
+    for (int h = 0; h < RING_MAX / 4; h++) {
+        if ((uint32_t)(h * 4) >= b.rdepth) break; /* wave-uniform */
+        const bool gh = go && slot0 == (uint32_t)(h * 4);
+        if (__any(gh)) { /* wave-uniform: the 4 DMAs below are issued exactly when this holds */
+            d += 4;
+            if (gh) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) dma_block(b, b.iend + k, (uint32_t)(h * 4 + k));
+            }
+        }
+    }
+    if (want) {
+        b.iend_old = b.iend;
+        if (go) b.iend += 4u;
+    }
+    q.s_prev = q.s_last;
+    q.s_last = 0;
+    q.d_last = d;
 }
 
 DEV uint64_t br_pos(const BR &b) { return ((uint64_t)(b.wi - 1u) << 5) - b.s; }
 DEV uint32_t br_peek(const BR &b) { return __builtin_amdgcn_alignbit(b.hi, b.lo, b.s); }
-DEV void br_adv(BR &b, uint32_t n) { /* n <= 32; branch-free except the rare landing check */
+/* Pending LDS store carried into the next cursor advance (fused decode): issuing it after
+ * the window update and before the next ring read keeps every LDS op covered by the next
+ * lgkmcnt wait a whole codeword old. */
+struct PendW {
+    int32_t *at;
+    int32_t v;
+    bool on;
+};
+DEV bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; } /* wave-uniform */
+
+template <bool CHECK = true>
+DEV void br_adv(BR &b, uint32_t n, PendW *pw = nullptr) { /* n <= 32; branch-free except the rare landing check */
     const int32_t t = (int32_t)b.s - (int32_t)n;
     const bool c = t < 0;
     b.s = (uint32_t)t & 31u;
     b.hi = c ? b.lo : b.hi;
     b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
     b.wi += c ? 1u : 0u;
-    if (__builtin_expect(__any(b.wi >= b.vendw), 0)) br_land(b);
-    /* issue the ring read after the window update, so the wait for the previous word
-     * (one codeword old) is not merged with a wait for this one */
-    __builtin_amdgcn_sched_barrier(0);
-    b.nx = ring_word(b, b.wi);
+    if (CHECK && __builtin_expect(any_lane(b.wi >= b.vendw), 0)) br_land(b);
+    if (pw && pw->on) *pw->at = pw->v;
+    /* issue the ring read after the window update (an artificial data dependency on the
+     * new lo), so the wait for the previous word (one codeword old) is not merged with a
+     * wait for this one; other instructions stay free to move */
+    uint32_t wi = b.wi;
+    asm volatile("" : "+v"(wi) : "v"(b.lo));
+    b.nx = ring_word(b, wi);
 }
 DEV uint32_t br_read(BR &b, uint32_t n) { /* 0..32 bits */
     uint32_t v = n ? (br_peek(b) >> ((32u - n) & 31u)) : 0u;
@@ -641,7 +730,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
 
 /* ================================================================== k_decode */
 #define DEC_LANES 64
-#define RP 68 /* row-buffer stride (dwords) between samples: [sample][lane], 16-byte skew */
+#define RP 72 /* row-buffer stride (dwords) between samples: [sample][lane]; 4*RP = 32 mod 64 banks */
 
 struct RS { /* residual reader state */
     uint32_t verb;   /* 1: VERBATIM raw values of `k` bits */
@@ -664,14 +753,14 @@ DEV void read_partition(BR &b, RS &s) {
 
 /* One Rice codeword (the block reader @0x10001b30/@0x1001aed0: u = (q << k) | lsb in
  * 32-bit unsigned, zig-zag). */
-DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc) {
+DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc, PendW *pw = nullptr) {
     const uint32_t w = br_peek(b);
     const uint32_t q0 = w ? (uint32_t)__builtin_clz(w) : 32u; /* v_ffbh + v_min */
     const uint32_t len = q0 + 1u + k;
     const bool fast = len <= 32u;
     uint32_t u = (q0 << k) | __builtin_amdgcn_ubfe(w, 31u - q0 - k, k);
-    br_adv(b, fast ? len : 0u);
-    if (__builtin_expect(__any(!fast), 0)) { /* wave-uniform test; the work is per lane */
+    br_adv(b, fast ? len : 0u, pw);
+    if (__builtin_expect(any_lane(!fast), 0)) { /* wave-uniform test; the work is per lane */
         STAT(b.stats, 3);
         if (!fast) { /* long unary prefix: read_unary_unsigned, then the k low bits */
             uint32_t q;
@@ -703,9 +792,18 @@ DEV void finish_partitions(BR &b, RS &s) {
     }
 }
 
-DEV int32_t sat16(int32_t x) { return min(max(x, -32768), 32767); }
+/* saturate to int16 (packssdw); the int16 round trip tells the compiler the value is a
+ * sign-extended 16-bit quantity, so v_mul_i32_i24 needs no re-extension */
+DEV int32_t sat16(int32_t x) { return (int32_t)(int16_t)min(max(x, -32768), 32767); }
 DEV int32_t tr16(int32_t x) { return (int32_t)(int16_t)(uint16_t)(uint32_t)x; }
-DEV int32_t mul24(int32_t a, int32_t b) { return ((a << 8) >> 8) * ((b << 8) >> 8); }
+/* low 32 bits of (sext24(a) * sext24(b)): one v_mul_i32_i24.  Written as asm because the
+ * C form ((a << 8) >> 8) * ((b << 8) >> 8) keeps a v_bfe per operand whenever the compiler
+ * cannot prove the operand already fits 24 bits (loop-carried history values). */
+DEV int32_t mul24(int32_t a, int32_t b) {
+    int32_t r;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 /* LPC prediction for the sample at ring position i (compile-time), libFLAC path P.
  * sh is the path's effective shift (MMX psrad: >= 32 -> 31; ia32 sar: & 31; 64-bit
@@ -779,16 +877,25 @@ DEV void lpc_chunk(int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t
 template <int CH, int W, int P, int N>
 DEV void lpc_fused(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
                    int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc) {
+    /* each sample's row write is issued just before the next codeword's ring read, so the
+     * next LDS wait (hipcc waits lgkmcnt(0) here) finds every LDS op a codeword old */
+    PendW pw;
+    pw.at = row;
+    pw.v = 0;
+    pw.on = false;
 #pragma unroll 1
     for (int j = 0; j < CH; j += W) {
 #pragma unroll
         for (int t = 0; t < W; t++) {
-            const int32_t r = rice_one(b, k, limit, trunc);
+            const int32_t r = rice_one(b, k, limit, trunc, &pw);
             const int32_t s = (int32_t)((uint32_t)r + (uint32_t)lpc_pred<W, P>(c, h, ht, t, sh));
             lpc_push<W, P>(h, ht, t, s);
-            row[(j + t) * RP] = (int32_t)((uint32_t)s << wasted);
+            pw.v = (int32_t)((uint32_t)s << wasted);
+            pw.at = row + (j + t) * RP;
+            pw.on = true;
         }
     }
+    *pw.at = pw.v;
 }
 
 /* FLAC__fixed_restore_signal @0x10003810 (ring of 8, 32-bit wrap) */
@@ -823,15 +930,22 @@ DEV void fixed_chunk(int32_t *row, int32_t (&h)[N], uint32_t n0, uint32_t nvalid
 template <int CH, int N>
 DEV void fixed_fused(BR &b, uint32_t k, int32_t *row, int32_t (&h)[N], uint32_t order, uint32_t wasted,
                      uint64_t limit, uint32_t &trunc) {
+    PendW pw;
+    pw.at = row;
+    pw.v = 0;
+    pw.on = false;
 #pragma unroll 1
     for (int j = 0; j < CH; j += 8) {
 #pragma unroll
         for (int t = 0; t < 8; t++) {
-            const uint32_t s = (uint32_t)rice_one(b, k, limit, trunc) + fixed_pred(h, t, order);
+            const uint32_t s = (uint32_t)rice_one(b, k, limit, trunc, &pw) + fixed_pred(h, t, order);
             h[t] = (int32_t)s;
-            row[(j + t) * RP] = (int32_t)(s << wasted);
+            pw.v = (int32_t)(s << wasted);
+            pw.at = row + (j + t) * RP;
+            pw.on = true;
         }
     }
+    *pw.at = pw.v;
 }
 
 /* CRC-16 (poly 0x8005) over bytes [b0, b1), slice-by-8 with the tables in LDS. */
@@ -899,44 +1013,50 @@ DEV void decorrelate(uint32_t as, int32_t &v0, int32_t &v1) {
 /* Pack one chunk: every lane writes a contiguous run of CH/chn_lanes samples of its own
  * frame (metadata in registers), reading the frame's channel rows from LDS.  Stereo
  * FLACDecoder / interleaved-int32 runs go out as 16-byte stores. */
+/* returns the path taken: 0 nothing stored, 1 vector fast path (pack_fast_stores<FMT,CH>
+ * store instructions), 2 generic per-sample path */
+template <int FMT, int CH> constexpr uint32_t pack_fast_stores() { return FMT == BNF_OUT_INTERLEAVED32 ? CH / 4 : CH / 8; }
 template <int FMT, int CH>
-DEV void pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, uint32_t n0, bool fok, uint32_t bs,
+DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, uint32_t n0, bool fok, uint32_t bs,
                    uint32_t C, uint32_t as, uint64_t os, uint32_t stream_channels, uint32_t fr_bytes,
                    uint8_t *__restrict__ out) {
     const uint32_t per = CH / chn_lanes;
     const uint32_t fl = lane / chn_lanes, part = lane % chn_lanes;
     const uint32_t i0 = part * per;
-    if (!fok || n0 + i0 >= bs) return;
+    if (!fok || n0 + i0 >= bs) return 0;
     const uint32_t cnt = min(per, bs - (n0 + i0));
     const int32_t *rows = lds + i0 * RP + fl * chn_lanes; /* channel c of sample q: rows[q * RP + c] */
     const uint64_t s0 = os + n0 + i0; /* first output sample of this run */
-    const uintptr_t dst = (uintptr_t)out + (uintptr_t)s0 * (FMT == BNF_OUT_INTERLEAVED32 ? 8u : 4u);
-    if ((FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_INTERLEAVED32) && C == 2 && chn_lanes == 2 && cnt == CH / 2 &&
-        (FMT == BNF_OUT_FLACDECODER || stream_channels == 2) && (dst & 15u) == 0) {
-        constexpr int PER = CH / 2;
-        int32_t l[PER], r[PER];
+    const uint32_t bpsmp = (FMT == BNF_OUT_INTERLEAVED32) ? 8u : 4u;
+    /* vector path (stereo): the frame's two lanes take interleaved 4-sample groups
+     * (lane h: samples 8g+4h .. 8g+4h+3), so each 16-byte store instruction writes 32
+     * contiguous bytes per frame */
+    const uintptr_t base = (uintptr_t)out + (uintptr_t)(os + n0) * bpsmp;
+    if ((FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_INTERLEAVED32) && C == 2 && chn_lanes == 2 && n0 + CH <= bs &&
+        (FMT == BNF_OUT_FLACDECODER || stream_channels == 2) && (base & 15u) == 0) {
+        const int32_t *frows = lds + fl * 2u; /* (L, R) of sample i at frows[i * RP] */
 #pragma unroll
-        for (int q = 0; q < PER; q++) {
-            const int2 v = *(const int2 *)(rows + q * RP); /* (L, R): lanes 2f, 2f+1 */
-            l[q] = v.x;
-            r[q] = v.y;
+        for (int g = 0; g < CH / 8; g++) {
+            const uint32_t i = 8u * g + 4u * part;
+            int32_t l[4], r[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int2 v = *(const int2 *)(frows + (i + q) * RP);
+                l[q] = v.x;
+                r[q] = v.y;
+                decorrelate(as, l[q], r[q]);
+            }
+            if (FMT == BNF_OUT_FLACDECODER) { /* FLACDecoder.cs:543-562: L | R << 16 */
+                *(uint4 *)(base + i * 4u) = make_uint4(((uint32_t)l[0] & 0xffffu) | ((uint32_t)r[0] << 16),
+                                                       ((uint32_t)l[1] & 0xffffu) | ((uint32_t)r[1] << 16),
+                                                       ((uint32_t)l[2] & 0xffffu) | ((uint32_t)r[2] << 16),
+                                                       ((uint32_t)l[3] & 0xffffu) | ((uint32_t)r[3] << 16));
+            } else {
+                *(int4 *)(base + i * 8u) = make_int4(l[0], r[0], l[1], r[1]);
+                *(int4 *)(base + i * 8u + 16u) = make_int4(l[2], r[2], l[3], r[3]);
+            }
         }
-#pragma unroll
-        for (int q = 0; q < PER; q++) decorrelate(as, l[q], r[q]);
-        if (FMT == BNF_OUT_FLACDECODER) { /* FLACDecoder.cs:543-562: L | R << 16 */
-            uint4 *o = (uint4 *)dst;
-#pragma unroll
-            for (int q = 0; q < PER; q += 4)
-                o[q / 4] = make_uint4(((uint32_t)l[q] & 0xffffu) | ((uint32_t)r[q] << 16),
-                                      ((uint32_t)l[q + 1] & 0xffffu) | ((uint32_t)r[q + 1] << 16),
-                                      ((uint32_t)l[q + 2] & 0xffffu) | ((uint32_t)r[q + 2] << 16),
-                                      ((uint32_t)l[q + 3] & 0xffffu) | ((uint32_t)r[q + 3] << 16));
-        } else {
-            int4 *o = (int4 *)dst;
-#pragma unroll
-            for (int q = 0; q < PER; q += 2) o[q / 2] = make_int4(l[q], r[q], l[q + 1], r[q + 1]);
-        }
-        return;
+        return 1;
     }
     for (uint32_t q = 0; q < cnt; q++) {
         const uint32_t n = n0 + i0 + q;
@@ -967,6 +1087,7 @@ DEV void pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, uint32
             }
         }
     }
+    return 2;
 }
 
 #define LPC_DISPATCH(FN, W_, ...)                                                                   \
@@ -1063,6 +1184,9 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
     br_init(b, words, nbytes, (lds_u32 *)ring, lane, RD);
     b.stats = (ablate & 0x100u) != 0;
     STAT(b.stats, 5);
+    const bool tmon = b.stats;
+    const uint64_t t_start = tnow(tmon);
+    uint64_t tm_dec = 0, tm_ref = 0, tm_pack = 0;
     SubHdr h;
     h.type = T_CONST; h.order = 0; h.wasted = 0; h.bps = 0; h.shift = 0; h.path = P_IA32; h.cval = 0;
     h.porder = 0; h.rice2 = 0;
@@ -1135,9 +1259,14 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
     const uint32_t nchunks = (mybs + CHK - 1) / CHK;
     const uint32_t W = h.order <= 8 ? 8u : (h.order <= 16 ? 16u : 32u);
 
+    const uint64_t t_loop = tnow(tmon);
+    wait_vm(); /* setup loads done: the pipeline counts start from zero */
+    VmQ vq;
+    vq.d_last = vq.s_last = vq.s_prev = 0;
     for (uint32_t kc = 0; kc < nchunks; kc++) {
         const uint32_t n0 = kc * CHK;
         const uint32_t nvalid = (active && n0 < bs) ? min((uint32_t)CHK, bs - n0) : 0u;
+        const uint64_t ta = tnow(tmon);
         if (nvalid) {
             bool fast = fast_ok && nvalid == CHK && n0 >= h.order;
             if (fast && rs.left == 0) {
@@ -1174,35 +1303,54 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
                     LPC_DISPATCH(lpc_chunk, W, row, c, hh, ht, n0, nvalid, h.order, sh, h.wasted);
                 }
             }
-            /* stage the next chunk's blocks now: the wait inside finds the previous DMAs
-             * and the previous chunk's PCM stores long done */
-            if (h.type != T_CONST && n0 + CHK < bs) {
-                STAT(b.stats, 4);
-                /* since the previous refill this wave issued only the last pack's stores
-                 * (CHK/8 16-byte stores on the stereo path): let those drain in the background */
-                br_refill<CHK / 8>(b);
-            }
+        }
+        const uint64_t tb = tnow(tmon);
+        /* stage the next chunk's blocks now: the wait inside finds the previous DMAs done.
+         * Since the previous refill this wave issued only the last pack's stores (CHK/8
+         * 16-byte stores on the stereo path): those keep draining in the background. */
+        {   /* whole wave: the vmcnt bookkeeping must stay uniform */
+            const bool want = nvalid && h.type != T_CONST && n0 + CHK < bs;
+            STAT(b.stats && want, 4);
+            br_refill2(b, want, vq, (ablate & 0x200u) != 0);
         }
         lds_sync();
+        const uint64_t tc = tnow(tmon);
+        tm_dec += tb - ta;
+        tm_ref += tc - tb;
+        uint32_t pk = 0, pkn = 0;
         switch ((ablate & 2u) ? -1 : fmt) {
         case -1:
             break;
         case BNF_OUT_PLANAR32:
-            pack_lane<BNF_OUT_PLANAR32, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
+            pk = pack_lane<BNF_OUT_PLANAR32, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
+            pkn = pack_fast_stores<BNF_OUT_PLANAR32, CHK>();
             break;
         case BNF_OUT_INTERLEAVED32:
-            pack_lane<BNF_OUT_INTERLEAVED32, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
+            pk = pack_lane<BNF_OUT_INTERLEAVED32, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
+            pkn = pack_fast_stores<BNF_OUT_INTERLEAVED32, CHK>();
             break;
         case BNF_OUT_FLACDECODER:
-            pack_lane<BNF_OUT_FLACDECODER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
+            pk = pack_lane<BNF_OUT_FLACDECODER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
+            pkn = pack_fast_stores<BNF_OUT_FLACDECODER, CHK>();
             break;
         default:
-            pack_lane<BNF_OUT_FILEREADER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels,
-                                                     sp.bps == 24 ? 3u : 2u, out);
+            pk = pack_lane<BNF_OUT_FILEREADER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels,
+                                                    sp.bps == 24 ? 3u : 2u, out);
+            pkn = pack_fast_stores<BNF_OUT_FILEREADER, CHK>();
             break;
         }
+        /* account this chunk's stores for the next refill's exact vmcnt wait: the vector
+         * path issues a fixed count; after the per-sample path, drain (rare) */
+        if (__any(pk == 2u)) {
+            wait_vm();
+            br_drained(b);
+        } else if (__any(pk == 1u)) {
+            vq.s_last += pkn;
+        }
         lds_sync();
+        tm_pack += tnow(tmon) - tc;
     }
+    const uint64_t t_loopend = tnow(tmon);
 
     /* ---- last subframe end, zero padding, CRC-16 (read_frame_ @0x100118c0 tail).  The
      * frame record is re-read here (only scalars stay live across the chunk loop). */
@@ -1286,6 +1434,14 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
         info[f] = fo;
     }
     __syncthreads();
+    if (tmon && lane == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memtime();
+        atomicAdd(&g_stats[8], (unsigned long long)(t_loop - t_start));
+        atomicAdd(&g_stats[9], (unsigned long long)tm_dec);
+        atomicAdd(&g_stats[10], (unsigned long long)tm_ref);
+        atomicAdd(&g_stats[11], (unsigned long long)tm_pack);
+        atomicAdd(&g_stats[12], (unsigned long long)(t_end - t_loopend));
+    }
     /* zero-fill CRC-failed frames' output */
     for (uint32_t fl2 = 0; fl2 < fpb; fl2++) {
         if (f_bad[fl2] != 2 || !f_ok[fl2]) continue;
@@ -1343,10 +1499,10 @@ static uint32_t ablate_flags() {
 
 void bnf_set_ablate(uint32_t v) { g_ablate = v; }
 
-hipError_t bnf_stats(uint64_t *out8, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stats), 8 * sizeof(uint64_t));
+hipError_t bnf_stats(uint64_t *out16, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stats), 16 * sizeof(uint64_t));
     if (e == hipSuccess && reset) {
-        static const uint64_t z[8] = {0};
+        static const uint64_t z[16] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z);
     }
     return e;
@@ -1368,7 +1524,7 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
     if (!nframes || !nbytes) return hipSuccess;
     const uint32_t fpb = DEC_LANES / chn_lanes;
     const dim3 grid((nframes + fpb - 1) / fpb);
-    hipLaunchKernelGGL((k_decode<8, 16, 4>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
+    hipLaunchKernelGGL((k_decode<8, 16, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
                        out_bytes, info, ablate_flags());
     hipLaunchKernelGGL((k_decode<32, 32, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
                        out_bytes, info, ablate_flags());

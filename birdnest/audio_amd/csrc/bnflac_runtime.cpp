@@ -40,7 +40,7 @@ hipError_t bnf_launch_sync_scan(const uint8_t *d, uint64_t n, uint32_t *d_block_
                                 uint64_t *d_out, uint32_t cap, hipStream_t s);
 uint32_t bnf_scan_blocks(uint64_t n);
 void bnf_set_ablate(uint32_t v);
-hipError_t bnf_stats(uint64_t *out8, int reset);
+hipError_t bnf_stats(uint64_t *out16, int reset);
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs,
                             uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
                             uint64_t base_sample, bnf_frame_info *info, hipStream_t s);
@@ -111,8 +111,8 @@ static int ensure_device(int dev) {
  * wrong while non-zero.  bit0 CRC-16, bit1 PCM stores, bit2 restore, bit3 Rice decode,
  * bit4 k_parse subframe walk. */
 extern "C" BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags) { bnf_set_ablate(flags); }
-extern "C" BNFLAC_API int bnflac_debug_stats(uint64_t *out8, int reset) {
-    return bnf_stats(out8, reset) == hipSuccess ? 0 : fail("bnflac_debug_stats failed");
+extern "C" BNFLAC_API int bnflac_debug_stats(uint64_t *out16, int reset) {
+    return bnf_stats(out16, reset) == hipSuccess ? 0 : fail("bnflac_debug_stats failed");
 }
 
 extern "C" BNFLAC_API int bnflac_device_count(void) {

@@ -152,10 +152,11 @@ BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uin
 /* Timing experiments only: skip parts of the kernels (bit0 CRC-16, bit1 PCM stores,
  * bit2 restore, bit3 Rice decode, bit4 subframe walk).  Output is wrong while set. */
 BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags);
-/* Debug: k_decode event counters collected while ablate bit 0x100 is set (fused chunks,
- * generic chunks, DMA landing waits, slow Rice codewords, refills, waves; wave-level
- * events).  Synchronous; reset != 0 clears them. */
-BNFLAC_API int bnflac_debug_stats(uint64_t *out8, int reset);
+/* Debug: k_decode event counters collected while ablate bit 0x100 is set: [0..5] fused
+ * chunks, generic chunks, DMA landing waits, slow Rice codewords, refills, waves (wave-level
+ * events); [8..12] shader-clock cycles summed over waves in setup, chunk decode, refill,
+ * pack, tail.  out16 holds 16 values.  Synchronous; reset != 0 clears them. */
+BNFLAC_API int bnflac_debug_stats(uint64_t *out16, int reset);
 
 /* Bytes of one sample frame (all channels of one sample index) in out_format. */
 BNFLAC_API uint32_t bnflac_out_stride(int out_format, const bnflac_stream_params *sp);
