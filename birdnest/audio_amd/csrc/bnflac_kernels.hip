@@ -1108,16 +1108,21 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
     } while (0)
 
 template <int MAXW, int CHK, int RD>
-__global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
+__global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
                                                       uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                       int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
                                                       bnf_frame_info *__restrict__ info, uint32_t ablate) {
     static_assert(MAXW <= CHK && CHK % 8 == 0 && RD <= RING_MAX, "chunk must hold the predictor ring");
     __shared__ uint32_t ring[RD * RING_LANE_DW];
     __shared__ int32_t lds[CHK * RP]; /* [sample][lane] */
-    __shared__ uint32_t f_bs[DEC_LANES], f_ch[DEC_LANES], f_as[DEC_LANES], f_ok[DEC_LANES];
-    __shared__ uint64_t f_out[DEC_LANES];
-    __shared__ uint32_t f_endbit[DEC_LANES], f_bad[DEC_LANES];
+    static_assert(CHK * RP >= 1024 + 448, "row buffer also holds the CRC tables and the tail's frame table");
+    /* per-frame tables overlay the buffers while those are idle: the setup exchange uses
+     * the ring before its first DMA, the tail uses the row buffer after the last pack */
+    uint32_t *f_bs = ring, *f_ch = ring + 64, *f_as = ring + 128, *f_ok = ring + 192;
+    uint64_t *f_out = (uint64_t *)(ring + 256);
+    uint32_t *t_bs = (uint32_t *)lds + 1024, *t_ch = t_bs + 64, *t_ok = t_bs + 128, *t_endbit = t_bs + 192,
+             *t_bad = t_bs + 256;
+    uint64_t *t_out = (uint64_t *)(t_bs + 320);
 
     const uint32_t lane = threadIdx.x;
     const uint32_t fpb = DEC_LANES / chn_lanes;
@@ -1133,7 +1138,7 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
     if ((MAXW == 32) != (__any(frame_ok && (fi.flags & BNF_FL_W32)) != 0)) return;
 
     bool active = frame_ok && ch < fi.channels && fi.channels <= chn_lanes;
-    if (lane < fpb) { f_ok[lane] = 0; f_bad[lane] = 0; f_bs[lane] = 0; }
+    if (lane < fpb) { f_ok[lane] = 0; f_bs[lane] = 0; }
     __syncthreads();
     if (have && ch == 0) {
         f_bs[fl] = frame_ok ? fi.blocksize : 0;
@@ -1177,6 +1182,7 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
     active = active && fok;
     const uint32_t fbs = fok ? f_bs[fl] : 0u, fch = have ? fi.channels : 0u, fas = fok ? f_as[fl] : 0u;
     const uint64_t fos = fok ? f_out[fl] : 0u;
+    lds_sync(); /* the ring's first DMA may overwrite the tables only after these reads */
     const uint64_t f_off = have ? fi.frame_off : 0u;
 
     /* ---- subframe setup */
@@ -1354,6 +1360,15 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
 
     /* ---- last subframe end, zero padding, CRC-16 (read_frame_ @0x100118c0 tail).  The
      * frame record is re-read here (only scalars stay live across the chunk loop). */
+    if (lane < fpb) { t_ok[lane] = 0; t_bad[lane] = 0; t_endbit[lane] = 0; }
+    lds_sync();
+    if (have && ch == 0) {
+        t_ok[fl] = fok ? 1u : 0u;
+        t_ch[fl] = fch;
+        t_bs[fl] = fbs;
+        t_out[fl] = fos;
+    }
+    lds_sync();
     const bool last = fok && frame_ok && ch + 1 == fch && fch <= chn_lanes;
     if (active) {
         finish_partitions(b, rs);
@@ -1389,14 +1404,14 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
                 if (br_pos(b) > limit) {
                     t_status = BNF_ST_TRUNC;
                 } else {
-                    f_endbit[fl] = (uint32_t)(end_byte - f_off);
+                    t_endbit[fl] = (uint32_t)(end_byte - f_off);
                     t_crc_read = crc_read;
                     t_resume = br_pos(b);
                     t_resume_set = true;
                 }
             }
         }
-        if (t_status != BNF_ST_OK) f_bad[fl] = 1;
+        if (t_status != BNF_ST_OK) t_bad[fl] = 1;
     }
     /* the rows are free now: stage the slice-by-8 CRC tables there */
     lds_u16 *T = (lds_u16 *)(lds_u32 *)lds;
@@ -1405,9 +1420,9 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
     /* CRC-16 over [frame_off, end): split across the frame's channel lanes, combined by
      * polynomial shifts (CRC is linear: crc(A|B) = crc(A)*x^(8|B|) + crc(B)). */
     uint32_t part = 0;
-    const bool crc_lane = fok && frame_ok && ch < fch && !f_bad[fl];
+    const bool crc_lane = fok && frame_ok && ch < fch && !t_bad[fl];
     if (crc_lane) {
-        const uint64_t len = f_endbit[fl];
+        const uint64_t len = t_endbit[fl];
         const uint32_t nl = fch;
         const uint64_t per = (len + nl - 1) / nl;
         const uint64_t s0 = f_off + min(len, per * ch), s1 = f_off + min(len, per * (ch + 1));
@@ -1429,7 +1444,7 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
             fo.crc16_read = t_crc_read;
             fo.crc16_calc = acc;
             fo.crc_ok = (acc == t_crc_read) ? 1u : 0u;
-            if (!fo.crc_ok) f_bad[fl] = 2; /* libFLAC zero-fills a CRC-failed frame (@0x10011af5) */
+            if (!fo.crc_ok) t_bad[fl] = 2; /* libFLAC zero-fills a CRC-failed frame (@0x10011af5) */
         }
         info[f] = fo;
     }
@@ -1444,16 +1459,16 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 4 : 1) k_decode(const u
     }
     /* zero-fill CRC-failed frames' output */
     for (uint32_t fl2 = 0; fl2 < fpb; fl2++) {
-        if (f_bad[fl2] != 2 || !f_ok[fl2]) continue;
+        if (t_bad[fl2] != 2 || !t_ok[fl2]) continue;
         uint64_t nbytes_fr, start;
-        const uint32_t C = f_ch[fl2], bsz = f_bs[fl2];
+        const uint32_t C = t_ch[fl2], bsz = t_bs[fl2];
         switch (fmt) {
-        case BNF_OUT_PLANAR32: start = f_out[fl2] * sp.channels * 4u; nbytes_fr = (uint64_t)C * bsz * 4u; break;
-        case BNF_OUT_INTERLEAVED32: start = f_out[fl2] * sp.channels * 4u; nbytes_fr = (uint64_t)sp.channels * bsz * 4u; break;
-        case BNF_OUT_FLACDECODER: start = f_out[fl2] * (C == 2 ? 4u : 2u); nbytes_fr = (uint64_t)bsz * (C == 2 ? 4u : 2u); break;
+        case BNF_OUT_PLANAR32: start = t_out[fl2] * sp.channels * 4u; nbytes_fr = (uint64_t)C * bsz * 4u; break;
+        case BNF_OUT_INTERLEAVED32: start = t_out[fl2] * sp.channels * 4u; nbytes_fr = (uint64_t)sp.channels * bsz * 4u; break;
+        case BNF_OUT_FLACDECODER: start = t_out[fl2] * (C == 2 ? 4u : 2u); nbytes_fr = (uint64_t)bsz * (C == 2 ? 4u : 2u); break;
         default: {
             const uint32_t fb = sp.bps == 24 ? 3u : 2u;
-            start = f_out[fl2] * sp.channels * fb;
+            start = t_out[fl2] * sp.channels * fb;
             nbytes_fr = (uint64_t)bsz * sp.channels * fb;
         }
         }
@@ -1524,7 +1539,7 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
     if (!nframes || !nbytes) return hipSuccess;
     const uint32_t fpb = DEC_LANES / chn_lanes;
     const dim3 grid((nframes + fpb - 1) / fpb);
-    hipLaunchKernelGGL((k_decode<8, 16, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
+    hipLaunchKernelGGL((k_decode<8, 32, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
                        out_bytes, info, ablate_flags());
     hipLaunchKernelGGL((k_decode<32, 32, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
                        out_bytes, info, ablate_flags());
