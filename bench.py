@@ -84,6 +84,21 @@ def cpu_baseline(data: bytes, nsamples_per_pass: int, budget_s: float, threads: 
     return passes * nsamples_per_pass / el / 1e6, passes, el
 
 
+def measured_traffic(B: int, frames: int, G: int):
+    """HBM bytes per k_decode launch from a committed PMC summary of this same workload
+    (profiles/traffic_c2_b<B>.json, written from tools/pmc_session.sh counters with the
+    MI355X_MICROARCH.md corrections).  PMC counters cannot be read from inside this run;
+    None when no summary matches the configuration."""
+    path = os.path.join(ROOT, "profiles", f"traffic_c2_b{B}.json")
+    if G != 1 or not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    if d.get("batches_per_step") != B or d.get("frames_per_batch") != frames:
+        return None
+    return {"traffic_bytes": int(d["traffic_bytes"]),
+            "source": f"profiles/{os.path.basename(path)} ({d.get('round', '?')}: FETCH_SIZE x2 + WRITE_SIZE)"}
+
+
 def cpu_model() -> str:
     try:
         for l in open("/proc/cpuinfo"):
@@ -286,7 +301,8 @@ def main():
                    "frames_per_batch": args.frames, "batches_per_step": B,
                    "compressed_bytes_per_batch": fb_in, "pcm_bytes_per_batch": pcm_bytes_per_batch,
                    "parallelism": f"frames sharded per rank x{world}",
-                   "pipeline": f"{G} groups of {B // G} batches: k_parse(g+1) || k_decode(g) on two streams"},
+                   "pipeline": (f"{G} groups of {B // G} batches: k_parse(g+1) || k_decode(g) on two streams"
+                                if G > 1 else "serial: k_parse then k_decode over all batches")},
         "bitexact": ok,
         "roofline": {"bound": "hbm", "kernel": "k_decode", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
@@ -294,6 +310,10 @@ def main():
                      "k_parse_avg_ms": round(t_parse, 4), "step_achieved_GBs": round(step_achieved, 1),
                      "launch": f"k_decode over one group ({B // G} batches x {args.frames} frames)"},
     }
+    tr = measured_traffic(B, args.frames, G)
+    if tr is not None:
+        line["roofline"]["traffic"] = tr["traffic_bytes"]
+        line["roofline"]["traffic_source"] = tr["source"]
     if args.stats and rank == 0:
         import ctypes
         buf = (ctypes.c_uint64 * 16)()
