@@ -125,10 +125,10 @@ DEV void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 DEV uint32_t gword(const BR &b, uint32_t w) { return (w < b.nw) ? b.w[w] : 0u; }
 /* ring layout [slot][lane][4 words] (16 bytes per lane per slot, the LDS-DMA dwordx4
  * image); block j lives in slot j % rdepth */
-DEV uint32_t ring_word(const BR &b, uint32_t w) {
-    const uint32_t t = w & b.wmask;
-    return b.lring[((t & ~3u) << 6) | (t & 3u)];
+DEV uint32_t ring_off(const BR &b, uint32_t w) { /* dword offset of word w from lring */
+    return ((w & (b.wmask & ~3u)) << 6) + (w & 3u);
 }
+DEV uint32_t ring_word(const BR &b, uint32_t w) { return b.lring[ring_off(b, w)]; }
 DEV void dma_block(const BR &b, uint32_t j, uint32_t slot) { /* one 16-byte block per lane */
     __builtin_amdgcn_global_load_lds((gvoid *)(b.w + (uint64_t)min(j, b.nblk - 1u) * 4u),
                                      (lds_void *)(b.ring + slot * RING_LANE_DW), 16, 0, 0);
@@ -236,6 +236,13 @@ struct PendW {
     bool on;
 };
 DEV bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; } /* wave-uniform */
+/* leading zeros, ~0u for 0 (v_ffbh_u32; asm so the compiler assumes no range) */
+DEV uint32_t ffbh(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 
 template <bool CHECK = true>
 DEV void br_adv(BR &b, uint32_t n, PendW *pw = nullptr) { /* n <= 32; branch-free except the rare landing check */
@@ -247,12 +254,12 @@ DEV void br_adv(BR &b, uint32_t n, PendW *pw = nullptr) { /* n <= 32; branch-fre
     b.wi += c ? 1u : 0u;
     if (CHECK && __builtin_expect(any_lane(b.wi >= b.vendw), 0)) br_land(b);
     if (pw && pw->on) *pw->at = pw->v;
-    /* issue the ring read after the window update (an artificial data dependency on the
-     * new lo), so the wait for the previous word (one codeword old) is not merged with a
-     * wait for this one; other instructions stay free to move */
-    uint32_t wi = b.wi;
-    asm volatile("" : "+v"(wi) : "v"(b.lo));
-    b.nx = ring_word(b, wi);
+    /* issue the ring read after the window update (an artificial data dependency of the
+     * address on the new lo), so the wait for the previous word (one codeword old) is not
+     * merged with a wait for this one; other instructions stay free to move */
+    uint32_t off = ring_off(b, b.wi);
+    asm volatile("" : "+v"(off) : "v"(b.lo));
+    b.nx = b.lring[off];
 }
 DEV uint32_t br_read(BR &b, uint32_t n) { /* 0..32 bits */
     uint32_t v = n ? (br_peek(b) >> ((32u - n) & 31u)) : 0u;
@@ -550,14 +557,14 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
             const uint32_t nb = br_read(b, 5);
             br_skip(b, (uint64_t)nb * cnt);
         } else {
-            const uint32_t k1 = k + 1u;
+            const uint32_t k1 = k + 1u, km = 31u - k;
             for (uint32_t i = 0; i < cnt; i++) {
                 if ((since++ & 31u) == 0 && !(ablate & 32u)) br_refill(b);
-                const uint32_t w = br_peek(b);
-                const uint32_t q = w ? (uint32_t)__builtin_clz(w) : 32u;
-                const bool fast = q + k1 <= 32u;
+                const uint32_t q = ffbh(br_peek(b)); /* ~0u for an empty window: slow */
+                const bool fast = q <= km;
+                const bool slow = any_lane(!fast);
                 br_adv(b, fast ? q + k1 : 0u);
-                if (__builtin_expect(__any(!fast), 0)) {
+                if (__builtin_expect(slow, 0)) {
                     if (!fast) {
                         uint32_t qq;
                         if (!br_unary(b, qq, limit)) return BNF_ST_TRUNC;
@@ -755,12 +762,14 @@ DEV void read_partition(BR &b, RS &s) {
  * 32-bit unsigned, zig-zag). */
 DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc, PendW *pw = nullptr) {
     const uint32_t w = br_peek(b);
-    const uint32_t q0 = w ? (uint32_t)__builtin_clz(w) : 32u; /* v_ffbh + v_min */
-    const uint32_t len = q0 + 1u + k;
-    const bool fast = len <= 32u;
-    uint32_t u = (q0 << k) | __builtin_amdgcn_ubfe(w, 31u - q0 - k, k);
-    br_adv(b, fast ? len : 0u, pw);
-    if (__builtin_expect(any_lane(!fast), 0)) { /* wave-uniform test; the work is per lane */
+    /* v_ffbh gives ~0u for w == 0, which fails the unsigned test below like any prefix
+     * too long for the window: the slow path then reads it */
+    const uint32_t q0 = ffbh(w);
+    const bool fast = q0 <= 31u - k;
+    uint32_t u = (q0 << k) | __builtin_amdgcn_ubfe(w, 31u - k - q0, k);
+    const bool slow = any_lane(!fast); /* wave-uniform, taken before the advance (stays in SGPRs) */
+    br_adv(b, fast ? q0 + 1u + k : 0u, pw);
+    if (__builtin_expect(slow, 0)) { /* the work is per lane */
         STAT(b.stats, 3);
         if (!fast) { /* long unary prefix: read_unary_unsigned, then the k low bits */
             uint32_t q;
@@ -804,6 +813,12 @@ DEV int32_t mul24(int32_t a, int32_t b) {
     asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+/* acc + low 32 bits of (sext24(a) * sext24(b)): one v_mad_i32_i24 (32-bit wrap add) */
+DEV int32_t mad24(int32_t a, int32_t b, int32_t acc) {
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(acc));
+    return r;
+}
 
 /* LPC prediction for the sample at ring position i (compile-time), libFLAC path P.
  * sh is the path's effective shift (MMX psrad: >= 32 -> 31; ia32 sar: & 31; 64-bit
@@ -815,7 +830,7 @@ DEV int32_t lpc_pred(const int32_t (&c)[N], const int32_t (&h)[N], const int32_t
 #pragma unroll
         for (int t = 0; t < W; t++) {
             const int32_t hv = (t < 4) ? ht[(i - 1 - t) & 3] : h[((i - 1 - t) % W + W) % W];
-            sum += mul24(c[t], hv);
+            sum = t ? mad24(c[t], hv, sum) : mul24(c[t], hv);
         }
         return sum >> sh;
     } else if (P == P_IA32) {
@@ -824,8 +839,8 @@ DEV int32_t lpc_pred(const int32_t (&c)[N], const int32_t (&h)[N], const int32_t
 #pragma unroll
         for (int t = 0; t < W; t++) {
             const int32_t hv = h[((i - 1 - t) % W + W) % W];
-            shi += mul24(c[t], hv >> 12);
-            slo += mul24(c[t], hv & 0xfff);
+            shi = t ? mad24(c[t], hv >> 12, shi) : mul24(c[t], hv >> 12);
+            slo = t ? mad24(c[t], hv & 0xfff, slo) : mul24(c[t], hv & 0xfff);
         }
         const int32_t sum = (int32_t)(((uint32_t)shi << 12) + (uint32_t)slo);
         return sum >> sh;
