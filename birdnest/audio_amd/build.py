@@ -39,15 +39,37 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+KERNEL_TUS = (0, 1, 2)  # bnflac_kernels.hip built once per BNF_TU: scan+parse, k_decode<8>, k_decode<32>
+
+
 def build_hip(force=False, verbose=False):
+    """Compile the kernel TUs and the runtime in parallel (hipcc -c), then link."""
     out = os.path.join(LIB, "libbnflac.so")
     if force or _stale(out, HIP_SOURCES + HIP_HEADERS):
         os.makedirs(LIB, exist_ok=True)
-        cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
-               "-I" + INCLUDE] + HIP_SOURCES + ["-o", out + ".tmp"]
+        objdir = os.path.join(PKG, "build")
+        os.makedirs(objdir, exist_ok=True)
+        base = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-I" + INCLUDE]
+        jobs, objs = [], []
+        for tu in KERNEL_TUS:
+            o = os.path.join(objdir, f"bnflac_kernels_tu{tu}.o")
+            jobs.append(base + [f"-DBNF_TU={tu}", "-c", HIP_SOURCES[0], "-o", o])
+            objs.append(o)
+        o = os.path.join(objdir, "bnflac_runtime.o")
+        jobs.append(base + ["-c", HIP_SOURCES[1], "-o", o])
+        objs.append(o)
+        procs = []
+        for cmd in jobs:
+            if verbose:
+                print(" ".join(cmd))
+            procs.append((cmd, subprocess.Popen(cmd)))
+        for cmd, p in procs:
+            if p.wait() != 0:
+                raise subprocess.CalledProcessError(p.returncode, cmd)
+        link = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"]
         if verbose:
-            print(" ".join(cmd))
-        subprocess.check_call(cmd)
+            print(" ".join(link))
+        subprocess.check_call(link)
         os.replace(out + ".tmp", out)
     return out
 

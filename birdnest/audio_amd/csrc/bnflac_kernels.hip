@@ -578,6 +578,7 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
     return BNF_ST_OK;
 }
 
+#if BNF_TU == 0
 /* =============================================================== k_sync_scan */
 #define SCAN_BYTES_PER_THREAD 16
 #define SCAN_THREADS 256
@@ -734,6 +735,8 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     fi.status = st;
     info[f] = fi;
 }
+
+#endif /* BNF_TU == 0 */
 
 /* ================================================================== k_decode */
 #define DEC_LANES 64
@@ -1492,14 +1495,76 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
 }
 
 /* ------------------------------------------------------------- host launchers */
-extern "C" {
-
-hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
+/* The library is built from this file three times (BNF_TU 0: sync scan + k_parse + shared
+ * launchers, 1: k_decode<8>, 2: k_decode<32>), so the instances compile in parallel.  Each
+ * TU is its own code object: the __constant__ tables are uploaded into every one. */
+static uint32_t g_ablate = 0xFFFFFFFFu;
+static uint32_t ablate_flags() {
+    if (g_ablate == 0xFFFFFFFFu) {
+        const char *e = getenv("BNFLAC_ABLATE"); /* timing experiments only: results are wrong */
+        g_ablate = e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+    }
+    return g_ablate;
+}
+static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc8_tab), crc8, 256);
     if (e != hipSuccess) return e;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_tab), crc16x8, 8 * 256 * sizeof(uint16_t));
     if (e != hipSuccess) return e;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_xpow), xpow, 40 * sizeof(uint16_t));
+}
+
+#if BNF_TU == 1 || BNF_TU == 2
+#define DEC_W (BNF_TU == 1 ? 8 : 32)
+#define TU_FN(name) TU_FN2(name, BNF_TU)
+#define TU_FN2(name, n) TU_FN3(name, n)
+#define TU_FN3(name, n) name##_tu##n
+extern "C" {
+hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
+    return upload_tables(crc8, crc16x8, xpow);
+}
+void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate = v; }
+hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
+    uint64_t v[16];
+    hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < 16; i++) out16[i] += v[i];
+    if (reset) {
+        static const uint64_t z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z);
+    }
+    return e;
+}
+hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
+                                    uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
+                                    hipStream_t s) {
+    const uint32_t fpb = DEC_LANES / chn_lanes;
+    const dim3 grid((nframes + fpb - 1) / fpb);
+    hipLaunchKernelGGL((k_decode<DEC_W, 32, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt,
+                       out, out_bytes, info, ablate_flags());
+    return hipGetLastError();
+}
+} /* extern "C" */
+#endif
+
+#if BNF_TU == 0
+extern "C" {
+hipError_t bnf_upload_tables_tu1(const uint8_t *, const uint16_t *, const uint16_t *);
+hipError_t bnf_upload_tables_tu2(const uint8_t *, const uint16_t *, const uint16_t *);
+void bnf_set_ablate_tu1(uint32_t);
+void bnf_set_ablate_tu2(uint32_t);
+hipError_t bnf_stats_tu1(uint64_t *, int);
+hipError_t bnf_stats_tu2(uint64_t *, int);
+hipError_t bnf_launch_decode_tu1(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                 uint64_t, bnf_frame_info *, hipStream_t);
+hipError_t bnf_launch_decode_tu2(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                 uint64_t, bnf_frame_info *, hipStream_t);
+
+hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
+    hipError_t e = upload_tables(crc8, crc16x8, xpow);
+    if (e == hipSuccess) e = bnf_upload_tables_tu1(crc8, crc16x8, xpow);
+    if (e == hipSuccess) e = bnf_upload_tables_tu2(crc8, crc16x8, xpow);
+    return e;
 }
 
 hipError_t bnf_launch_sync_scan(const uint8_t *d, uint64_t n, uint32_t *d_block_counts, uint32_t *d_total,
@@ -1518,24 +1583,16 @@ uint32_t bnf_scan_blocks(uint64_t n) {
     return (uint32_t)((n + per_block - 1) / per_block);
 }
 
-static uint32_t g_ablate = 0xFFFFFFFFu;
-static uint32_t ablate_flags() {
-    if (g_ablate == 0xFFFFFFFFu) {
-        const char *e = getenv("BNFLAC_ABLATE"); /* timing experiments only: results are wrong */
-        g_ablate = e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
-    }
-    return g_ablate;
+void bnf_set_ablate(uint32_t v) {
+    g_ablate = v;
+    bnf_set_ablate_tu1(v);
+    bnf_set_ablate_tu2(v);
 }
 
-void bnf_set_ablate(uint32_t v) { g_ablate = v; }
-
 hipError_t bnf_stats(uint64_t *out16, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stats), 16 * sizeof(uint64_t));
-    if (e == hipSuccess && reset) {
-        static const uint64_t z[16] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z);
-    }
-    return e;
+    for (int i = 0; i < 16; i++) out16[i] = 0;
+    hipError_t e = bnf_stats_tu1(out16, reset);
+    return e == hipSuccess ? bnf_stats_tu2(out16, reset) : e;
 }
 
 /* words: 16-byte aligned; the allocation must cover round_up(nbytes, 16) bytes. */
@@ -1552,18 +1609,14 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
                              uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
                              hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
-    const uint32_t fpb = DEC_LANES / chn_lanes;
-    const dim3 grid((nframes + fpb - 1) / fpb);
-    hipLaunchKernelGGL((k_decode<8, 32, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
-                       out_bytes, info, ablate_flags());
-    hipLaunchKernelGGL((k_decode<32, 32, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt, out,
-                       out_bytes, info, ablate_flags());
-    return hipGetLastError();
+    hipError_t e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
+    return e;
 }
 
 hipError_t bnf_launch_scan_u32(uint32_t *v, uint32_t n, uint32_t *total, hipStream_t s) {
     hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, v, n, total);
     return hipGetLastError();
 }
-
 } /* extern "C" */
+#endif
