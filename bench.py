@@ -40,7 +40,9 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batches", type=int, default=256, help="C2 batches (x1024 frames) decoded per step")
+    ap.add_argument("--batches", type=int, default=192,
+                    help="C2 batches (x1024 frames) decoded per step; 192 = one k_decode_st wave (64 frames) "
+                         "per resident slot (256 CUs x 12 waves)")
     ap.add_argument("--frames", type=int, default=1024, help="frames per batch (BASELINE C2: 1024)")
     ap.add_argument("--groups", type=int, default=1,
                     help="pipeline groups: k_parse of group g+1 overlaps k_decode of group g (1 = serial)")

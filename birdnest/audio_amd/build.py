@@ -39,7 +39,7 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-KERNEL_TUS = (0, 1, 2)  # bnflac_kernels.hip built once per BNF_TU: scan+parse, k_decode<8>, k_decode<32>
+KERNEL_TUS = (0, 1, 2, 3, 4)  # one build of bnflac_kernels.hip per BNF_TU: scan+parse, k_decode<8>, k_decode<32>, k_decode_st<FLACDECODER>, k_decode_st<others>
 
 
 def build_hip(force=False, verbose=False):
@@ -51,9 +51,14 @@ def build_hip(force=False, verbose=False):
         os.makedirs(objdir, exist_ok=True)
         base = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-I" + INCLUDE]
         jobs, objs = [], []
+        # development shortcut: BNFLAC_DEV_TUS="1,3" recompiles only those kernel TUs and
+        # reuses the other objects as they are (never set for a real build)
+        dev = os.environ.get("BNFLAC_DEV_TUS")
+        only = {int(x) for x in dev.split(",")} if dev else None
         for tu in KERNEL_TUS:
             o = os.path.join(objdir, f"bnflac_kernels_tu{tu}.o")
-            jobs.append(base + [f"-DBNF_TU={tu}", "-c", HIP_SOURCES[0], "-o", o])
+            if only is None or tu in only or not os.path.exists(o):
+                jobs.append(base + [f"-DBNF_TU={tu}", "-c", HIP_SOURCES[0], "-o", o])
             objs.append(o)
         o = os.path.join(objdir, "bnflac_runtime.o")
         jobs.append(base + ["-c", HIP_SOURCES[1], "-o", o])

@@ -65,6 +65,27 @@ DEV uint64_t tnow(bool on) { /* call at wave-uniform points only */
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) void lds_void;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+/* LDS accesses to buffers that are never LDS-DMA targets, as inline asm: hipcc cannot tell
+ * them from the DMA'd ring and would drain every vector-memory op (vmcnt(0)) first.
+ * Completion is waited for explicitly (lds_sync / lgkmcnt). */
+DEV void lds_st128(const void *a, u32x4 v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"((uint32_t)(uintptr_t)a), "v"(v) : "memory");
+}
+DEV u32x4 lds_ld128(const void *a) { /* result valid after s_waitcnt lgkmcnt(0) */
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)a) : "memory");
+    return v;
+}
+DEV void lds_st64(const void *a, uint64_t v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"((uint32_t)(uintptr_t)a), "v"(v) : "memory");
+}
+DEV uint64_t lds_ld64(const void *a) {
+    uint64_t v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)a) : "memory");
+    return v;
+}
 typedef __attribute__((address_space(1))) const void gvoid;
 
 /* ----------------------------------------------------------------- bit reader */
@@ -85,6 +106,7 @@ struct BR {
     uint32_t wi, s, hi, lo, nx;
     uint32_t vendw, iend;           /* words < vendw landed in the ring; blocks < iend issued */
     uint32_t iend_old;              /* k_decode's 2-deep DMA pipeline: issued two refills ago */
+    uint32_t ra, vlim;              /* k_decode_st: ring byte address of word wi (with the lane's bits), vendw - 1 */
     bool stats;
 };
 
@@ -141,8 +163,9 @@ template <int KEEP = 0> /* KEEP: younger vector-memory ops (PCM stores) that may
 DEV void br_refill(BR &b) {
     wait_vm_but<KEEP>();
     b.vendw = b.iend * 4u;
-    /* whole 64-byte lines: [iend, first line of the cursor + rdepth) */
-    const uint32_t need = (b.wi >> 2) & ~3u;
+    /* whole 64-byte lines: [iend, first line of the cursor + rdepth); a 4-slot ring (one
+     * line) refills from the cursor's block instead */
+    const uint32_t need = b.rdepth >= 8u ? ((b.wi >> 2) & ~3u) : (b.wi >> 2);
     const uint32_t lo = max(b.iend, need), hi = need + b.rdepth;
 #pragma unroll
     for (int s = 0; s < RING_MAX; s++) {
@@ -731,6 +754,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
             }
         }
         if (maxorder > 8) fi.flags |= BNF_FL_W32;
+        else if (fi.channels == 2) fi.flags |= BNF_FL_ST;
     }
     fi.status = st;
     info[f] = fi;
@@ -1151,6 +1175,8 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
     bnf_frame_info fi;
     bool have = (fl < fpb) && (f < nframes);
     if (have) fi = info[f];
+    /* stereo frames are k_decode_st's, unless it handed them back (BNF_FL_REDO) */
+    if (have && (fi.flags & BNF_FL_ST) && !(fi.flags & BNF_FL_REDO) && !(ablate & 0x400u)) have = false;
     const bool frame_ok = have && fi.status == BNF_ST_OK;
     /* one wave per workgroup: the W=8 and W=32 instances split the blocks between them */
     if ((MAXW == 32) != (__any(frame_ok && (fi.flags & BNF_FL_W32)) != 0)) return;
@@ -1494,6 +1520,658 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
     }
 }
 
+#if BNF_TU == 3 || BNF_TU == 4
+/* =============================================================== k_decode_st
+ * Stereo fast path: one lane per 2-channel frame (both subframes, two independent bit
+ * cursors), 64 frames per single-wave workgroup.  Same arithmetic as k_decode (read_frame_
+ * @0x100118c0 and below) and the same PCM layouts (A15/A17), but:
+ *   - the two channels' Rice + predictor chains interleave in one lane (ILP 2);
+ *   - decorrelation (@0x10011a37-0x10011adb) and the PCM pack happen in registers, so
+ *     there is no row buffer in LDS (LDS = the two bitstream rings, 16 KB per wave);
+ *   - FIXED (@0x10003810), LPC MMX-16 and LPC ia32 restores share one predictor: eight
+ *     v_mad_i32_i24 over the raw history.  That is exact while every history value fits
+ *     the path's operand range (16 bits: MMX packssdw/pmaddwd see the sample itself; 24
+ *     bits: the 24x24 multiply is the exact low 32 bits of the ia32 imul).  Each channel
+ *     tracks its sample range; a frame that leaves it is handed back.
+ * Frames it declines (VERBATIM/CONSTANT/64-bit-path subframes, errors, truncation, CRC
+ * mismatch, out-of-range samples, unsupported layouts) get BNF_FL_REDO and are decoded
+ * again, exactly, by k_decode<8>, which runs after it on the same stream. */
+#define ST_CHK 16 /* samples per chunk (one 64-byte FLACDecoder run per frame) */
+#define ST_RD 4  /* 16-byte ring slots per lane and channel */
+
+struct StCh {
+    BR b;
+    int32_t c[8], h[8]; /* predictor coefficients (0 past the order) and history ring */
+    int32_t sh;         /* effective shift of the libFLAC path */
+    uint32_t k, km, k1, k32; /* Rice parameter, 31 - k, k + 1, 32 - k */
+    uint32_t esc, left, pidx, nparts, psamples, plen, pesc, porder, order;
+    uint32_t wasted;
+    int32_t lim, mx, mn; /* operand range of the path, sample range seen */
+};
+
+/* subframe header -> fast-path state; false: hand the frame back */
+DEV bool st_setup(StCh &z, uint32_t bps, uint32_t bs, uint64_t limit) {
+    SubHdr h;
+    int32_t warm[8], coef[8], err = -1;
+    const uint32_t st = parse_subframe_head<true, 8>(z.b, bps, bs, limit, h, warm, coef, err);
+    if (st != BNF_ST_OK) return false;
+    if (h.type != T_FIXED && h.type != T_LPC) return false;
+    if (h.type == T_LPC && (h.order > 8 || h.path == P_WIDE)) return false;
+    if (h.bps > 24) return false;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        z.c[t] = 0;
+        z.h[t] = ((uint32_t)t < h.order) ? warm[t] : 0;
+    }
+    z.sh = 0;
+    z.lim = 0x7FFFFF;
+    if (h.type == T_LPC) {
+#pragma unroll
+        for (int t = 0; t < 8; t++) z.c[t] = ((uint32_t)t < h.order) ? coef[t] : 0;
+        if (h.path == P_MMX16) {
+            z.sh = ((uint32_t)h.shift >= 32u) ? 31 : h.shift;
+            z.lim = 0x7FFF;
+        } else {
+            z.sh = h.shift & 31;
+        }
+    } else { /* FIXED order o as LPC: 1 | 2,-1 | 3,-3,1 | 4,-6,4,-1 (32-bit wrap, shift 0) */
+        const uint32_t o = h.order;
+        z.c[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
+        z.c[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
+        z.c[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
+        z.c[3] = o == 4 ? -1 : 0;
+    }
+    z.order = h.order;
+    z.wasted = h.wasted;
+    z.porder = h.porder;
+    z.nparts = 1u << h.porder;
+    z.psamples = h.porder ? bs >> h.porder : bs - h.order;
+    z.plen = h.rice2 ? 5u : 4u;
+    z.pesc = h.rice2 ? 31u : 15u;
+    z.left = 0;
+    z.pidx = 0;
+    z.esc = 0;
+    z.k = 0;
+    z.km = 31;
+    z.k1 = 1;
+    z.k32 = 32;
+    z.mx = 0;
+    z.mn = 0;
+    return true;
+}
+
+DEV void st_partition(StCh &z) { /* read_residual_partitioned_rice_ @0x10012da0 */
+    const uint32_t kk = br_read(z.b, z.plen);
+    z.left = (z.porder == 0 || z.pidx > 0) ? z.psamples : z.psamples - z.order;
+    if (kk < z.pesc) {
+        z.k = kk;
+        z.esc = 0;
+    } else {
+        z.k = br_read(z.b, 5);
+        z.esc = 1;
+    }
+    z.km = 31u - z.k;
+    z.k1 = z.k + 1u;
+    z.k32 = 32u - z.k;
+    z.pidx++;
+}
+
+/* every DMA issued before the wave's `nst` youngest vector-memory ops has landed */
+DEV void st_land(BR &b, uint32_t nst) {
+    STAT(b.stats, 2);
+    wait_vm_n(nst);
+    b.vendw = b.iend * 4u;
+    if (b.wi >= b.vendw) { /* outran the whole ring: blocking refill (rare) */
+        br_refill(b);
+        wait_vm();
+        br_drained(b);
+    }
+}
+
+/* branch-free advance by n <= 32 bits; the landing check waits only for the DMAs */
+DEV void st_adv(BR &b, uint32_t n, uint32_t nst) {
+    const int32_t t = (int32_t)b.s - (int32_t)n;
+    const bool c = t < 0;
+    b.s = (uint32_t)t & 31u;
+    b.hi = c ? b.lo : b.hi;
+    b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
+    b.wi += c ? 1u : 0u;
+    if (__builtin_expect(any_lane(b.wi >= b.vendw), 0)) st_land(b, nst);
+    uint32_t off = ring_off(b, b.wi);
+    asm volatile("" : "+v"(off) : "v"(b.lo));
+    b.nx = b.lring[off];
+}
+
+/* one Rice codeword of a non-escaped partition (@0x10001b30 semantics, zig-zag) */
+DEV int32_t st_rice(StCh &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
+    const uint32_t w = br_peek(z.b);
+    const uint32_t q = ffbh(w); /* ~0u for an empty window: slow */
+    const bool slow = q >= z.k32; /* prefix + stop bit + k bits overrun the 32-bit window */
+    uint32_t u = (q << z.k) | __builtin_amdgcn_ubfe(w, z.km - q, z.k);
+    const bool anyslow = any_lane(slow);
+    st_adv(z.b, slow ? 0u : q + z.k1, nst);
+    if (__builtin_expect(anyslow, 0)) {
+        STAT(z.b.stats, 3);
+        if (slow) {
+            uint32_t qq;
+            if (!br_unary(z.b, qq, limit)) trunc = 1;
+            u = (qq << z.k) | br_read(z.b, z.k);
+        }
+    }
+    return (int32_t)((u >> 1) ^ (0u - (u & 1u)));
+}
+
+/* next residual, any partition state (warm-up excluded) */
+DEV int32_t st_next(StCh &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
+    while (z.left == 0) {
+        if (z.pidx >= z.nparts) {
+            trunc = 1;
+            return 0;
+        }
+        st_partition(z);
+    }
+    z.left--;
+    if (z.esc) return br_read_s(z.b, z.k);
+    return st_rice(z, limit, trunc, nst);
+}
+
+/* sum_j c[j] * h[i-1-j] (32-bit wrap, 24x24-bit products) for both channels, interleaved
+ * in one asm block (no hazard padding between the dependent multiply-adds) */
+template <int I>
+DEV void st_dot2(const StCh &a, const StCh &b, int32_t &pa, int32_t &pb) {
+#define H_(z, j) z.h[(I + 7 - (j)) & 7]
+    asm("v_mul_i32_i24 %0, %2, %18\n\t"
+        "v_mul_i32_i24 %1, %10, %26\n\t"
+        "v_mad_i32_i24 %0, %3, %19, %0\n\t"
+        "v_mad_i32_i24 %1, %11, %27, %1\n\t"
+        "v_mad_i32_i24 %0, %4, %20, %0\n\t"
+        "v_mad_i32_i24 %1, %12, %28, %1\n\t"
+        "v_mad_i32_i24 %0, %5, %21, %0\n\t"
+        "v_mad_i32_i24 %1, %13, %29, %1\n\t"
+        "v_mad_i32_i24 %0, %6, %22, %0\n\t"
+        "v_mad_i32_i24 %1, %14, %30, %1\n\t"
+        "v_mad_i32_i24 %0, %7, %23, %0\n\t"
+        "v_mad_i32_i24 %1, %15, %31, %1\n\t"
+        "v_mad_i32_i24 %0, %8, %24, %0\n\t"
+        "v_mad_i32_i24 %1, %16, %32, %1\n\t"
+        "v_mad_i32_i24 %0, %9, %25, %0\n\t"
+        "v_mad_i32_i24 %1, %17, %33, %1"
+        : "=&v"(pa), "=&v"(pb)
+        : "v"(a.c[0]), "v"(a.c[1]), "v"(a.c[2]), "v"(a.c[3]), "v"(a.c[4]), "v"(a.c[5]), "v"(a.c[6]), "v"(a.c[7]),
+          "v"(b.c[0]), "v"(b.c[1]), "v"(b.c[2]), "v"(b.c[3]), "v"(b.c[4]), "v"(b.c[5]), "v"(b.c[6]), "v"(b.c[7]),
+          "v"(H_(a, 0)), "v"(H_(a, 1)), "v"(H_(a, 2)), "v"(H_(a, 3)), "v"(H_(a, 4)), "v"(H_(a, 5)), "v"(H_(a, 6)), "v"(H_(a, 7)),
+          "v"(H_(b, 0)), "v"(H_(b, 1)), "v"(H_(b, 2)), "v"(H_(b, 3)), "v"(H_(b, 4)), "v"(H_(b, 5)), "v"(H_(b, 6)), "v"(H_(b, 7)));
+#undef H_
+}
+
+/* The seven older taps of the NEXT sample's prediction, sum_{j=1..7} c[j] * h[T-j], from
+ * the history as it stands at step T (both channels interleaved): off the critical path,
+ * so only c[0] * s_T remains between consecutive samples (st_fin2). */
+template <int T>
+DEV void st_pre2(const StCh &a, const StCh &b, int32_t &pa, int32_t &pb) {
+#define P_(z, j) z.h[(T + 8 - (j)) & 7]
+    asm("v_mul_i32_i24 %0, %2, %16\n\t"
+        "v_mul_i32_i24 %1, %9, %23\n\t"
+        "v_mad_i32_i24 %0, %3, %17, %0\n\t"
+        "v_mad_i32_i24 %1, %10, %24, %1\n\t"
+        "v_mad_i32_i24 %0, %4, %18, %0\n\t"
+        "v_mad_i32_i24 %1, %11, %25, %1\n\t"
+        "v_mad_i32_i24 %0, %5, %19, %0\n\t"
+        "v_mad_i32_i24 %1, %12, %26, %1\n\t"
+        "v_mad_i32_i24 %0, %6, %20, %0\n\t"
+        "v_mad_i32_i24 %1, %13, %27, %1\n\t"
+        "v_mad_i32_i24 %0, %7, %21, %0\n\t"
+        "v_mad_i32_i24 %1, %14, %28, %1\n\t"
+        "v_mad_i32_i24 %0, %8, %22, %0\n\t"
+        "v_mad_i32_i24 %1, %15, %29, %1"
+        : "=&v"(pa), "=&v"(pb)
+        : "v"(a.c[1]), "v"(a.c[2]), "v"(a.c[3]), "v"(a.c[4]), "v"(a.c[5]), "v"(a.c[6]), "v"(a.c[7]),
+          "v"(b.c[1]), "v"(b.c[2]), "v"(b.c[3]), "v"(b.c[4]), "v"(b.c[5]), "v"(b.c[6]), "v"(b.c[7]),
+          "v"(P_(a, 1)), "v"(P_(a, 2)), "v"(P_(a, 3)), "v"(P_(a, 4)), "v"(P_(a, 5)), "v"(P_(a, 6)), "v"(P_(a, 7)),
+          "v"(P_(b, 1)), "v"(P_(b, 2)), "v"(P_(b, 3)), "v"(P_(b, 4)), "v"(P_(b, 5)), "v"(P_(b, 6)), "v"(P_(b, 7)));
+#undef P_
+}
+/* pred = c[0] * h + pre for both channels (the critical-path tap) */
+DEV void st_fin2(const StCh &a, const StCh &b, int32_t ha, int32_t hb, int32_t prea, int32_t preb, int32_t &pa,
+                 int32_t &pb) {
+    asm("v_mad_i32_i24 %0, %2, %4, %6\n\t"
+        "v_mad_i32_i24 %1, %3, %5, %7"
+        : "=&v"(pa), "=&v"(pb)
+        : "v"(a.c[0]), "v"(b.c[0]), "v"(ha), "v"(hb), "v"(prea), "v"(preb));
+}
+
+DEV void st_range(StCh &z, int32_t s0, int32_t s1) {
+    z.mx = max(z.mx, max(s0, s1));
+    z.mn = min(z.mn, min(s0, s1));
+}
+
+/* Channel decorrelation of 4 sample pairs; wave-uniform assignment takes a scalar branch */
+DEV void st_decor4(bool uni, uint32_t as_u, uint32_t as, int32_t (&L)[4], int32_t (&R)[4]) {
+    const uint32_t a = uni ? as_u : as;
+    if (a == 1) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) R[q] = (int32_t)((uint32_t)L[q] - (uint32_t)R[q]);
+    } else if (a == 2) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) L[q] = (int32_t)((uint32_t)L[q] + (uint32_t)R[q]);
+    } else if (a == 3) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t side = (uint32_t)R[q], mid = ((uint32_t)L[q] << 1) | (side & 1u);
+            L[q] = (int32_t)(mid + side) >> 1;
+            R[q] = (int32_t)(mid - side) >> 1;
+        }
+    }
+}
+
+/* Pack and store samples n..n+3 of this lane's frame (nv of them valid); returns whether
+ * this lane issued a store.  dst: the frame's first byte in the layout (planar: channel 0). */
+template <int FMT>
+DEV bool st_emit4(uint8_t *dst, uint32_t n, uint32_t nv, bool al, uint32_t bs, const int32_t (&L)[4],
+                  const int32_t (&R)[4]) {
+    if (nv == 0) return false;
+    if (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER) { /* 16-bit L | R << 16 */
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_perm((uint32_t)R[q], (uint32_t)L[q], 0x05040100u);
+        uint32_t *o = (uint32_t *)(dst + (uint64_t)n * 4u);
+        if (al && nv == 4) *(uint4 *)o = make_uint4(w[0], w[1], w[2], w[3]);
+        else
+            for (uint32_t q = 0; q < nv; q++) o[q] = w[q];
+    } else if (FMT == BNF_OUT_INTERLEAVED32) {
+        int32_t *o = (int32_t *)(dst + (uint64_t)n * 8u);
+        if (al && nv == 4) {
+            *(int4 *)o = make_int4(L[0], R[0], L[1], R[1]);
+            *(int4 *)(o + 4) = make_int4(L[2], R[2], L[3], R[3]);
+        } else {
+            for (uint32_t q = 0; q < nv; q++) { o[2 * q] = L[q]; o[2 * q + 1] = R[q]; }
+        }
+    } else { /* PLANAR32: channel 0 then channel 1, bs samples each */
+        int32_t *o0 = (int32_t *)dst + n, *o1 = (int32_t *)dst + bs + n;
+        if (al && nv == 4) {
+            *(int4 *)o0 = make_int4(L[0], L[1], L[2], L[3]);
+            *(int4 *)o1 = make_int4(R[0], R[1], R[2], R[3]);
+        } else {
+            for (uint32_t q = 0; q < nv; q++) { o0[q] = L[q]; o1[q] = R[q]; }
+        }
+    }
+    return true;
+}
+
+/* 1-deep ring pipeline, 16-byte granular: every lane keeps its ring full -- the blocks from
+ * its cursor's block up to 8 ahead -- so after the next refill's wait ~5 blocks (~20 words)
+ * are landed ahead of each cursor, more than a chunk consumes at CD bit rates.  One exec-
+ * masked LDS-DMA per ring slot that some lane needs.  Whole wave. */
+DEV void st_refill_issue(BR &b, bool want) {
+    const uint32_t need = b.wi >> 2; /* block holding the cursor's next word */
+    const uint32_t lo = max(b.iend, need), hi = need + ST_RD;
+#pragma unroll
+    for (int s = 0; s < ST_RD; s++) {
+        const uint32_t j = lo + (((uint32_t)s - lo) & (ST_RD - 1u));
+        if (want && j < hi) dma_block(b, j, (uint32_t)s);
+    }
+    if (want) b.iend = max(b.iend, hi);
+}
+
+/* CRC-16 of [b0, b1) with two 64-byte loads in flight (tables in LDS) */
+DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
+    uint32_t crc = 0;
+    uint64_t p = b0;
+    while (p < b1 && (p & 63u)) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
+    const uint4 *q = (const uint4 *)(bytes + p);
+    const uint32_t nl = (uint32_t)((b1 - p) >> 6); /* whole 64-byte lines */
+    if (nl) {
+        uint4 cur[4], nxt[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) cur[u] = q[u];
+        for (uint32_t i = 0; i < nl; i++) {
+            const uint32_t j = min(i + 1u, nl - 1u);
+#pragma unroll
+            for (int u = 0; u < 4; u++) nxt[u] = q[4u * j + u];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                crc = crc16_step8(crc, __builtin_bswap32(cur[u].x), __builtin_bswap32(cur[u].y), T);
+                crc = crc16_step8(crc, __builtin_bswap32(cur[u].z), __builtin_bswap32(cur[u].w), T);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) cur[u] = nxt[u];
+        }
+    }
+    p += (uint64_t)nl * 64u;
+    while (p < b1) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
+    return crc;
+}
+
+/* Fused-path cursor (4-slot ring).  ra is the LDS byte offset of ring word wi inside the
+ * channel's ring: bits 2-3 word in block, 4-9 lane, 10-11 slot.  Moving it one word on is
+ * ((ra | 0x3F3) + c) & 0xC0C | lane bits: the ones in bits 0-1 turn +c into +4, the ones in
+ * bits 4-9 carry a block wrap into the slot. */
+DEV uint32_t st_ra(uint32_t wi, uint32_t lane) { return ((wi & 3u) << 2) | (lane << 4) | (((wi >> 2) & 3u) << 10); }
+/* Advance by n <= 32 bits without the landing check: s - n borrows exactly when the window
+ * moves on a word, and that borrow steps wi and ra (v_sub_co / v_addc). */
+DEV void st_adv_nc(BR &b, uint32_t n, uint32_t laneb) {
+    uint32_t t;
+    const bool c = __builtin_usub_overflow(b.s, n, &t);
+    b.s = t & 31u;
+    b.hi = c ? b.lo : b.hi;
+    b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
+    b.wi += (uint32_t)c;
+    b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0xC0Cu) | laneb;
+}
+DEV void st_next_word(BR &b) { b.nx = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + b.ra); }
+DEV void st_resync(BR &b, uint32_t lane) { /* after generic-reader moves: ra, vlim from wi, vendw */
+    b.ra = st_ra(b.wi, lane);
+    b.vlim = b.vendw - 1u;
+}
+/* rare cases of a fused step, per channel: the cursor entered ring words not known to have
+ * landed (wait for the DMAs, read the word again), or a unary prefix too long for the window
+ * (the lane did not advance: decode the codeword with the generic reader) */
+DEV void st_rare(StCh &z, bool sl, bool ld, uint32_t &u, uint64_t limit, uint32_t &trunc, uint32_t nst,
+                uint32_t lane) {
+    if (any_lane(ld)) {
+        st_land(z.b, nst); /* lands the next two words (the check runs every other step) */
+        if (z.b.wi + 1u >= z.b.vendw) { /* the word after wi is beyond the ring: refill (rare) */
+            wait_vm();
+            br_refill(z.b);
+            wait_vm();
+            br_drained(z.b);
+        }
+        st_next_word(z.b);
+    }
+    if (any_lane(sl)) {
+        STAT(z.b.stats, 3);
+        if (sl) {
+            uint32_t qq;
+            if (!br_unary(z.b, qq, limit)) trunc = 1;
+            u = (qq << z.k) | br_read(z.b, z.k);
+        }
+    }
+    st_resync(z.b, lane);
+}
+
+/* One sample of both channels on the fused path (T: position in the 8-sample group).  The
+ * two channels' predictor sums, Rice decodes and cursor advances form one basic block (a
+ * single wave-uniform branch to the rare cases), so their dependency chains interleave.
+ * STG: the 16-bit stereo layouts, whose packed words go to the LDS staging tile (stg: this
+ * lane's 64-byte row, rotated by (lane >> 2) & 3 16-byte units: conflict-free both for the
+ * per-lane b128 writes and for the frame-contiguous b128 reads of the flush); other layouts
+ * store directly. */
+template <int T, int FMT>
+DEV void st_fused_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
+                       uint32_t nq, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al,
+                       uint32_t bs, bool store, lds_u32 *stg, uint32_t rot, uint32_t gq, int32_t &pre0, int32_t &pre1,
+                       uint32_t lane, bool anyw) {
+    constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
+    constexpr uint32_t spg = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u;
+    const uint32_t nqt = nq + ((!STG && T >= 4 && store) ? spg : 0u); /* + this group's direct store */
+    int32_t p0, p1, n0, n1;
+    st_fin2(z0, z1, z0.h[(T + 7) & 7], z1.h[(T + 7) & 7], pre0, pre1, p0, p1); /* this sample's prediction */
+    st_pre2<T>(z0, z1, n0, n1);                                                /* the next one's older taps */
+    pre0 = n0;
+    pre1 = n1;
+    const uint32_t w0 = br_peek(z0.b), w1 = br_peek(z1.b);
+    const uint32_t q0 = ffbh(w0), q1 = ffbh(w1); /* ~0u for an empty window: slow */
+    const bool sl0 = q0 >= z0.k32, sl1 = q1 >= z1.k32; /* prefix + stop bit + k bits overrun the window */
+    uint32_t u0 = (q0 << z0.k) | __builtin_amdgcn_ubfe(w0, z0.km - q0, z0.k);
+    uint32_t u1 = (q1 << z1.k) | __builtin_amdgcn_ubfe(w1, z1.km - q1, z1.k);
+    const uint32_t laneb = lane << 4;
+    st_adv_nc(z0.b, sl0 ? 0u : q0 + z0.k1, laneb);
+    st_adv_nc(z1.b, sl1 ? 0u : q1 + z1.k1, laneb);
+    /* landing check on even steps only: the words read now and at the next step must have
+     * landed (wi advances by at most one word per step) */
+    const bool ld0 = (T & 1) == 0 && z0.b.wi >= z0.b.vlim, ld1 = (T & 1) == 0 && z1.b.wi >= z1.b.vlim;
+    st_next_word(z0.b);
+    st_next_word(z1.b);
+    if (__builtin_expect(any_lane(sl0 || sl1 || ld0 || ld1), 0)) {
+        st_rare(z0, sl0, ld0, u0, limit, trunc, nqt, lane);
+        st_rare(z1, sl1, ld1, u1, limit, trunc, nqt, lane);
+    }
+    const int32_t s0 = (int32_t)(((u0 >> 1) ^ (0u - (u0 & 1u))) + (uint32_t)(p0 >> z0.sh));
+    const int32_t s1 = (int32_t)(((u1 >> 1) ^ (0u - (u1 & 1u))) + (uint32_t)(p1 >> z1.sh));
+    if (T & 1) {
+        st_range(z0, z0.h[(T + 7) & 7], s0);
+        st_range(z1, z1.h[(T + 7) & 7], s1);
+    }
+    z0.h[T] = s0;
+    z1.h[T] = s1;
+    L[T & 3] = s0;
+    R[T & 3] = s1;
+    if ((T & 3) == 3) {
+        if (__builtin_expect(anyw, 0)) { /* wasted bits (wave-uniform test) */
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                L[q] = (int32_t)((uint32_t)L[q] << z0.wasted);
+                R[q] = (int32_t)((uint32_t)R[q] << z1.wasted);
+            }
+        }
+        st_decor4(as_uni, as_u, as, L, R);
+        if (STG) {
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_perm((uint32_t)R[q], (uint32_t)L[q], 0x05040100u);
+            const uint32_t u = (gq + (uint32_t)(T >> 2) + rot) & 3u; /* 16-byte unit in the row */
+            lds_st128((const void *)(stg + 4u * u), u32x4{w[0], w[1], w[2], w[3]});
+        } else if (store) {
+            st_emit4<FMT>(dst, nbase + (uint32_t)T - 3u, 4u, al, bs, L, R);
+        }
+    }
+}
+
+/* One sample of both channels on the general path: warm-up, partition headers anywhere,
+ * escaped partitions, the frame's last partial chunk.  Returns whether a store was issued. */
+template <int T, int FMT>
+DEV bool st_gen_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
+                     uint32_t nst, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t n, bool valid,
+                     bool al, uint32_t bs, bool store) {
+    const bool v = valid && n < bs;
+    int32_t s0 = 0, s1 = 0;
+    if (v) {
+        int32_t p0, p1;
+        st_dot2<T>(z0, z1, p0, p1);
+        if (n < z0.order) s0 = z0.h[T];
+        else s0 = (int32_t)((uint32_t)st_next(z0, limit, trunc, nst) + (uint32_t)(p0 >> z0.sh));
+        if (n < z1.order) s1 = z1.h[T];
+        else s1 = (int32_t)((uint32_t)st_next(z1, limit, trunc, nst) + (uint32_t)(p1 >> z1.sh));
+        st_range(z0, s0, s0);
+        st_range(z1, s1, s1);
+        z0.h[T] = s0;
+        z1.h[T] = s1;
+    }
+    L[T & 3] = (int32_t)((uint32_t)s0 << z0.wasted);
+    R[T & 3] = (int32_t)((uint32_t)s1 << z1.wasted);
+    bool stored = false;
+    if ((T & 3) == 3) {
+        const uint32_t nq = n - 3u;
+        const uint32_t nv = (valid && nq < bs) ? min(4u, bs - nq) : 0u;
+        st_decor4(as_uni, as_u, as, L, R);
+        if (store) stored = st_emit4<FMT>(dst, nq, nv, al, bs, L, R);
+    }
+    return stored;
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict__ words, uint64_t nbytes,
+                                                     uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
+                                                     uint8_t *__restrict__ out, uint64_t out_bytes,
+                                                     bnf_frame_info *__restrict__ info, uint32_t ablate) {
+    constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
+    constexpr uint32_t ST_SPG = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u; /* stores per 4 samples */
+    __shared__ uint32_t ring[2 * ST_RD * RING_LANE_DW]; /* 8 KB: both channels' bitstream rings */
+    __shared__ uint32_t stg_tile[64 * 16];              /* 4 KB: one 64-byte PCM run per frame */
+    __shared__ uint64_t fdst[64];                       /* this chunk's run address per frame (0: none) */
+    const uint32_t lane = threadIdx.x;
+    const uint32_t f = blockIdx.x * 64u + lane;
+    const uint64_t limit = nbytes * 8u;
+    bnf_frame_info fi;
+    const bool have = f < nframes;
+    if (have) fi = info[f];
+    const bool mine = have && fi.status == BNF_ST_OK && (fi.flags & BNF_FL_ST) && !(fi.flags & BNF_FL_REDO);
+    if (!__any(mine)) return;
+
+    /* layouts this kernel writes; anything else (and every skip rule of k_decode's setup)
+     * goes back to k_decode<8> */
+    uint64_t stride = 0;
+    bool ok = mine && fi.channels == 2 && chn_lanes >= 2;
+    if (FMT == BNF_OUT_FLACDECODER) { stride = 4; ok = ok && fi.bps == 16 && sp.channels >= 2; }
+    else if (FMT == BNF_OUT_FILEREADER) { stride = 4; ok = ok && sp.channels == 2 && sp.bps == 16; }
+    else if (FMT == BNF_OUT_INTERLEAVED32) { stride = 8; ok = ok && sp.channels == 2; }
+    else { stride = 4ull * sp.channels; ok = ok && sp.channels == 2; }
+    const uint32_t bs = ok ? fi.blocksize : 0u;
+    const uint64_t os = ok ? fi.out_sample : 0u;
+    ok = ok && (os + bs) * stride <= out_bytes;
+    uint8_t *dst = out + os * stride; /* the frame's first byte (planar: channel 0's) */
+    const bool al = (((uintptr_t)dst) & 15u) == 0 && (FMT != BNF_OUT_PLANAR32 || (bs & 3u) == 0);
+
+    StCh z0, z1;
+    lds_u32 *ring0 = (lds_u32 *)ring, *ring1 = (lds_u32 *)ring + ST_RD * RING_LANE_DW;
+    br_init(z0.b, words, nbytes, ring0, lane, ST_RD);
+    br_init(z1.b, words, nbytes, ring1, lane, ST_RD);
+    z0.b.stats = z1.b.stats = (ablate & 0x100u) != 0;
+    STAT(z0.b.stats, 5);
+    if (ok) {
+        const uint64_t fbit = fi.frame_off * 8u;
+        br_seek(z0.b, fbit + fi.sub_start[0]);
+        ok = st_setup(z0, sub_bps(fi, 0), bs, limit);
+    }
+    if (ok) {
+        br_seek(z1.b, fi.frame_off * 8u + fi.sub_start[1]);
+        ok = st_setup(z1, sub_bps(fi, 1), bs, limit);
+    }
+    const uint32_t as = ok ? fi.assignment : 0u;
+    const bool anyw = any_lane(ok && (z0.wasted | z1.wasted) != 0u);
+    const uint32_t as_u = __builtin_amdgcn_readfirstlane(as);
+    const bool as_uni = !any_lane(ok && as != as_u);
+    /* staging: this lane's row (write side), and the flush's frame / unit (read side) */
+    lds_u32 *stg_row = (lds_u32 *)stg_tile + lane * 16u;
+    const uint32_t rot = (lane >> 2) & 3u;
+    const uint32_t fl_unit = lane & 3u;
+
+    uint32_t mybs = ok ? bs : 0u;
+    for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
+    const uint32_t nchunks = (mybs + ST_CHK - 1) / ST_CHK;
+    uint32_t trunc = 0;
+    wait_vm(); /* setup loads done: the store count starts from zero */
+    uint32_t nst = 0; /* vector-memory ops (PCM stores) issued by this wave since the last refill's DMAs */
+    for (uint32_t kc = 0; kc < nchunks; kc++) {
+        const uint32_t n0 = kc * ST_CHK;
+        const bool valid = ok && n0 < bs;
+        bool fast = valid && n0 >= 8u && n0 + ST_CHK <= bs && !(ablate & 12u);
+        if (fast) { /* partition headers at the chunk boundary (aligned partitions) */
+            if (z0.left == 0 && z0.pidx < z0.nparts) st_partition(z0);
+            if (z1.left == 0 && z1.pidx < z1.nparts) st_partition(z1);
+            fast = !z0.esc && !z1.esc && z0.left >= ST_CHK && z1.left >= ST_CHK;
+        }
+        const bool fused = !any_lane(valid && !fast);
+        if (fused) {
+            if (valid) {
+                STAT(z0.b.stats, 0);
+                int32_t pre0, pre1;
+                st_pre2<7>(z0, z1, pre0, pre1); /* older taps of the chunk's first sample */
+                st_resync(z0.b, lane);
+                st_resync(z1.b, lane);
+#pragma unroll 1
+                for (uint32_t g = 0; g < ST_CHK / 8; g++) {
+                    int32_t L[4], R[4];
+                    const uint32_t nq = nst + (STG ? 0u : g * 2u * ST_SPG); /* stores issued since the DMAs (at least) */
+                    const uint32_t nb = n0 + g * 8u;
+                    const bool sto = !(ablate & 2u);
+#define FSTEP(T) st_fused_step<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, stg_row, rot, 2u * g, pre0, pre1, lane, anyw)
+                    FSTEP(0); FSTEP(1); FSTEP(2); FSTEP(3); FSTEP(4); FSTEP(5); FSTEP(6); FSTEP(7);
+#undef FSTEP
+                }
+                z0.left -= ST_CHK;
+                z1.left -= ST_CHK;
+            }
+            if (!STG && !(ablate & 2u) && any_lane(valid)) nst += (ST_CHK / 4) * ST_SPG;
+            if (STG) lds_st64((const void *)&fdst[lane], (valid && !(ablate & 2u)) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull);
+        } else {
+            STAT(z0.b.stats, 1);
+#pragma unroll 1
+            for (uint32_t g = 0; g < ST_CHK / 8; g++) {
+                int32_t L[4], R[4];
+                const uint32_t nb = n0 + g * 8u;
+                const bool sto = !(ablate & 2u);
+                bool st0, st1;
+#define GSTEP(T) st_gen_step<T, FMT>(z0, z1, L, R, limit, trunc, nst, as_uni, as_u, as, dst, nb + T, valid, al, bs, sto)
+                GSTEP(0); GSTEP(1); GSTEP(2);
+                st0 = GSTEP(3);
+                if (any_lane(st0)) nst += 1u; /* at least one store instruction */
+                GSTEP(4); GSTEP(5); GSTEP(6);
+                st1 = GSTEP(7);
+                if (any_lane(st1)) nst += 1u;
+#undef GSTEP
+            }
+        }
+        /* refill before the flush: wait for the previous refill's DMAs (every store since
+         * stays in flight), then issue the next blocks; the flush's stores are younger */
+        {
+            const bool want = valid && n0 + ST_CHK < bs;
+            wait_vm_n(nst);
+            z0.b.vendw = z0.b.iend * 4u;
+            z1.b.vendw = z1.b.iend * 4u;
+            st_refill_issue(z0.b, want);
+            st_refill_issue(z1.b, want);
+            nst = 0;
+        }
+        if (STG && fused) { /* flush: 4 lanes per frame, one 64-byte run each, 16 frames per store */
+            lds_sync();
+            uint64_t a[4];
+            u32x4 v[4];
+#pragma unroll
+            for (uint32_t r = 0; r < 4; r++) {
+                const uint32_t fr = 16u * r + (lane >> 2);
+                a[r] = lds_ld64((const void *)&fdst[fr]);
+                v[r] = lds_ld128((const void *)((lds_u32 *)stg_tile + fr * 16u + 4u * ((fl_unit + (fr >> 2)) & 3u)));
+            }
+            lds_sync(); /* reads landed; the next chunk's staging writes come after them */
+#pragma unroll
+            for (uint32_t r = 0; r < 4; r++) {
+                if (a[r]) *(u32x4 *)((uint8_t *)(uintptr_t)a[r] + 16u * fl_unit) = v[r];
+                if (any_lane(a[r] != 0)) nst += 1u;
+            }
+        }
+    }
+
+    /* ---- end of the last subframe, zero padding, CRC-16 (read_frame_ tail) */
+    uint32_t crc_read = 0;
+    uint64_t end_byte = 0, resume = 0;
+    if (ok) {
+        if (z0.mx > z0.lim || z0.mn < -z0.lim - 1 || z1.mx > z1.lim || z1.mn < -z1.lim - 1) ok = false;
+        if (trunc) ok = false;
+    }
+    if (ok) {
+        while (z1.pidx < z1.nparts) { /* finish_partitions */
+            const uint32_t kk = br_read(z1.b, z1.plen);
+            if (kk >= z1.pesc) br_read(z1.b, 5);
+            z1.pidx++;
+        }
+        const uint32_t padbits = (uint32_t)((8u - (br_pos(z1.b) & 7u)) & 7u);
+        const uint32_t zp = br_read(z1.b, padbits);
+        if (br_pos(z1.b) > limit || zp != 0) ok = false;
+        end_byte = br_pos(z1.b) >> 3;
+        crc_read = br_read(z1.b, 16);
+        if (br_pos(z1.b) > limit) ok = false;
+        resume = br_pos(z1.b);
+    }
+    wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
+    lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
+    for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
+    __syncthreads();
+    uint32_t crc = 0;
+    if (ok && !(ablate & 1u)) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
+    if ((ablate & 1u) && ok) crc = crc_read;
+    if (ok && crc != crc_read) ok = false;
+    if (ok) {
+        info[f].resume_bit = resume;
+        info[f].crc16_read = crc_read;
+        info[f].crc16_calc = crc;
+        info[f].crc_ok = 1u;
+    } else if (mine) {
+        info[f].flags = fi.flags | BNF_FL_REDO;
+    }
+}
+#endif /* BNF_TU == 3 || BNF_TU == 4 */
+
 /* ------------------------------------------------------------- host launchers */
 /* The library is built from this file three times (BNF_TU 0: sync scan + k_parse + shared
  * launchers, 1: k_decode<8>, 2: k_decode<32>), so the instances compile in parallel.  Each
@@ -1514,11 +2192,11 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
     return hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_xpow), xpow, 40 * sizeof(uint16_t));
 }
 
-#if BNF_TU == 1 || BNF_TU == 2
-#define DEC_W (BNF_TU == 1 ? 8 : 32)
 #define TU_FN(name) TU_FN2(name, BNF_TU)
 #define TU_FN2(name, n) TU_FN3(name, n)
 #define TU_FN3(name, n) name##_tu##n
+#if BNF_TU == 1 || BNF_TU == 2
+#define DEC_W (BNF_TU == 1 ? 8 : 32)
 extern "C" {
 hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     return upload_tables(crc8, crc16x8, xpow);
@@ -1547,8 +2225,64 @@ hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint
 } /* extern "C" */
 #endif
 
+#if BNF_TU == 3 || BNF_TU == 4
+/* TU 3: k_decode_st<FLACDECODER>; TU 4: the other layouts */
+extern "C" {
+hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
+    return upload_tables(crc8, crc16x8, xpow);
+}
+void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate = v; }
+hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
+    uint64_t v[16];
+    hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < 16; i++) out16[i] += v[i];
+    if (reset) {
+        static const uint64_t z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z);
+    }
+    return e;
+}
+/* stereo fast path; launched before k_decode<8> (it hands frames back to it) */
+hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
+                                    uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
+                                    hipStream_t s) {
+    const dim3 grid((nframes + 63) / 64);
+    const uint32_t ab = ablate_flags();
+    if (ab & 0x400u) return hipSuccess; /* timing ablation: everything to k_decode<8> */
+#if BNF_TU == 3
+    (void)fmt;
+    hipLaunchKernelGGL(k_decode_st<BNF_OUT_FLACDECODER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, ab);
+#else
+    switch (fmt) {
+    case BNF_OUT_PLANAR32:
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_PLANAR32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, ab);
+        break;
+    case BNF_OUT_INTERLEAVED32:
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_INTERLEAVED32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, ab);
+        break;
+    default:
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_FILEREADER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, ab);
+        break;
+    }
+#endif
+    return hipGetLastError();
+}
+} /* extern "C" */
+#endif
+
 #if BNF_TU == 0
 extern "C" {
+hipError_t bnf_upload_tables_tu3(const uint8_t *, const uint16_t *, const uint16_t *);
+hipError_t bnf_upload_tables_tu4(const uint8_t *, const uint16_t *, const uint16_t *);
+void bnf_set_ablate_tu3(uint32_t);
+void bnf_set_ablate_tu4(uint32_t);
+hipError_t bnf_stats_tu3(uint64_t *, int);
+hipError_t bnf_stats_tu4(uint64_t *, int);
+hipError_t bnf_launch_decode_tu3(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                 uint64_t, bnf_frame_info *, hipStream_t);
+hipError_t bnf_launch_decode_tu4(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                 uint64_t, bnf_frame_info *, hipStream_t);
 hipError_t bnf_upload_tables_tu1(const uint8_t *, const uint16_t *, const uint16_t *);
 hipError_t bnf_upload_tables_tu2(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu1(uint32_t);
@@ -1564,6 +2298,8 @@ hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const
     hipError_t e = upload_tables(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu1(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu2(crc8, crc16x8, xpow);
+    if (e == hipSuccess) e = bnf_upload_tables_tu3(crc8, crc16x8, xpow);
+    if (e == hipSuccess) e = bnf_upload_tables_tu4(crc8, crc16x8, xpow);
     return e;
 }
 
@@ -1587,12 +2323,16 @@ void bnf_set_ablate(uint32_t v) {
     g_ablate = v;
     bnf_set_ablate_tu1(v);
     bnf_set_ablate_tu2(v);
+    bnf_set_ablate_tu3(v);
+    bnf_set_ablate_tu4(v);
 }
 
 hipError_t bnf_stats(uint64_t *out16, int reset) {
     for (int i = 0; i < 16; i++) out16[i] = 0;
     hipError_t e = bnf_stats_tu1(out16, reset);
-    return e == hipSuccess ? bnf_stats_tu2(out16, reset) : e;
+    if (e == hipSuccess) e = bnf_stats_tu2(out16, reset);
+    if (e == hipSuccess) e = bnf_stats_tu3(out16, reset);
+    return e == hipSuccess ? bnf_stats_tu4(out16, reset) : e;
 }
 
 /* words: 16-byte aligned; the allocation must cover round_up(nbytes, 16) bytes. */
@@ -1609,7 +2349,10 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
                              uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
                              hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
-    hipError_t e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
+    hipError_t e = fmt == BNF_OUT_FLACDECODER
+                       ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s)
+                       : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
     if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
     return e;
 }

@@ -267,3 +267,63 @@ def test_stream_api_large_c2_windows(gpu):
     oev, opcm = oracle.run(s.data.tobytes(), driver=1)
     assert ev == harness.oracle_events_as_tuples(oev)
     assert np.array_equal(pcm, opcm)
+
+
+# ------------------------------------------------ stereo fast path (k_decode_st)
+FL_ST, FL_REDO = 32, 64
+
+
+@pytest.mark.parametrize("fmt_name", ["OUT_FLACDECODER", "OUT_INTERLEAVED32", "OUT_PLANAR32", "OUT_FILEREADER"])
+@pytest.mark.parametrize("cfg,kw", [("C1", {}), ("C2", {}), ("C2", {"stereo_mode": 1}), ("C2", {"stereo_mode": 2}),
+                                    ("C2", {"stereo_mode": 3}), ("C2", {"partition_order": 0}),
+                                    ("C2", {"blocksize": 1152}), ("C1", {"blocksize": 4000})])
+def test_stereo_fast_path_layouts(gpu, fmt_name, cfg, kw):
+    """k_decode_st (one lane per stereo frame) writes every layout bit-exactly, and takes
+    the frames itself (BNF_FL_ST set, no hand-back) on regular streams -- including a
+    blocksize that is not a multiple of its 32-sample chunk (general path for the tail)."""
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    fmt = getattr(libflac, fmt_name)
+    p = synth.config(cfg, nframes=70, last_blocksize=0, **kw)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    out, info, sp = _decode_batch(gpu, data, s.frame_offsets, fmt)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    assert (info["flags"] & FL_ST).all(), info["flags"]
+    assert not (info["flags"] & FL_REDO).any(), info["flags"]
+    pcm = s.pcm.astype(np.int64)
+    if fmt == libflac.OUT_INTERLEAVED32:
+        assert np.array_equal(out.view("<i4").reshape(-1, 2), s.pcm)
+    elif fmt == libflac.OUT_PLANAR32:
+        got = out.view("<i4")
+        o = 0
+        for fr in range(p.nframes):
+            bs = int(info["blocksize"][fr])
+            st = int(info["out_sample"][fr])
+            assert np.array_equal(got[o: o + 2 * bs].reshape(2, bs).T, s.pcm[st: st + bs])
+            o += 2 * bs
+    else:
+        assert out.tobytes() == (pcm & 0xFFFF).astype("<u2").tobytes()
+    ev, opcm = oracle.run(data)
+    assert np.array_equal(s.pcm, oracle.interleave(ev, opcm))
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C4"])
+def test_stereo_handback_matches(gpu, cfg):
+    """With k_decode_st disabled (ablation 0x400) every stereo frame goes to k_decode<8>;
+    both routes give identical PCM and frame records."""
+    from birdnest.audio_amd import synth
+    torch, libflac, dec = gpu
+    p = synth.config(cfg, nframes={"C4": 64}.get(cfg, 16), last_blocksize=0)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    out_a, info_a, _ = _decode_batch(gpu, data, s.frame_offsets, libflac.OUT_FLACDECODER)
+    dec.L.bnflac_debug_set_ablate(0x400)
+    try:
+        out_b, info_b, _ = _decode_batch(gpu, data, s.frame_offsets, libflac.OUT_FLACDECODER)
+    finally:
+        dec.L.bnflac_debug_set_ablate(0)
+    assert out_a.tobytes() == out_b.tobytes()
+    keep = [n for n in info_a.dtype.names if n != "flags"]
+    assert all(np.array_equal(info_a[n], info_b[n]) for n in keep)
