@@ -579,6 +579,34 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
         if (k >= pesc) {
             const uint32_t nb = br_read(b, 5);
             br_skip(b, (uint64_t)nb * cnt);
+        } else if (!(ablate & 64u)) {
+            /* two codewords per 32-bit window when both fit: the second's prefix is counted in
+             * the window shifted past the first (zeros shifted in can only make it not fit) */
+            const uint32_t k1 = k + 1u, km = 31u - k;
+            uint32_t rem = cnt;
+            while (any_lane(rem != 0u)) {
+                if (any_lane((since++ & 15u) == 0u) && !(ablate & 32u)) br_refill(b);
+                if (rem != 0u) {
+                    const uint32_t w = br_peek(b);
+                    const uint32_t q1 = ffbh(w); /* ~0u for an empty window */
+                    const bool fit1 = q1 <= km;
+                    const uint32_t len1 = q1 + k1;
+                    const uint32_t room = 32u - len1;
+                    const uint32_t q2 = ffbh(w << (len1 & 31u));
+                    const bool fit2 = fit1 && rem >= 2u && len1 < 32u && q2 < room && q2 + k1 <= room;
+                    const bool slow = any_lane(!fit1);
+                    br_adv(b, fit2 ? len1 + q2 + k1 : (fit1 ? len1 : 0u));
+                    rem -= fit2 ? 2u : (fit1 ? 1u : 0u);
+                    if (__builtin_expect(slow, 0)) {
+                        if (!fit1) {
+                            uint32_t qq;
+                            if (!br_unary(b, qq, limit)) return BNF_ST_TRUNC;
+                            br_adv(b, k);
+                            rem--;
+                        }
+                    }
+                }
+            }
         } else {
             const uint32_t k1 = k + 1u, km = 31u - k;
             for (uint32_t i = 0; i < cnt; i++) {

@@ -23,3 +23,5 @@ for f in range(len(ia)):
     if nd or f < 3:
         print(f, "st", ia["status"][f], ib["status"][f], "flags", ia["flags"][f], ib["flags"][f], "bs", ia["blocksize"][f],
               "os", ia["out_sample"][f], "as", ia["assignment"][f], "crc", ia["crc_ok"][f], ib["crc_ok"][f], "nd", nd)
+import collections
+print("flags histogram (ST run):", collections.Counter(int(x) for x in ia["flags"]))
