@@ -19,7 +19,7 @@ LIB = os.path.join(PKG, "lib")
 INCLUDE = os.path.join(ROOT, "include")
 
 HIP_SOURCES = [os.path.join(CSRC, "bnflac_kernels.hip"), os.path.join(CSRC, "bnflac_runtime.cpp")]
-HIP_HEADERS = [os.path.join(CSRC, "bnflac_device.h"), os.path.join(INCLUDE, "bnflac.h"),
+HIP_HEADERS = [os.path.join(CSRC, "bnflac_device.h"), os.path.join(CSRC, "bnflac_md5.h"), os.path.join(INCLUDE, "bnflac.h"),
                os.path.join(INCLUDE, "FLAC_compat.h")]
 SYNTH_SOURCES = [os.path.join(CSRC, "synth", "bnflac_synth.c")]
 SYNTH_HEADERS = [os.path.join(CSRC, "synth", "bnflac_synth.h")]

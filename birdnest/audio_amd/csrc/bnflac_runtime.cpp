@@ -25,6 +25,7 @@
 
 #include "../../../include/bnflac.h"
 #include "bnflac_device.h"
+#include "bnflac_md5.h"
 
 static_assert(sizeof(bnflac_frame_info) == sizeof(bnf_frame_info), "frame info layout");
 static_assert(sizeof(bnf_frame_info) == 128, "frame info is 128 bytes");
@@ -158,6 +159,20 @@ extern "C" BNFLAC_API uint32_t bnflac_out_stride(int fmt, const bnflac_stream_pa
     }
 }
 
+extern "C" BNFLAC_API int bnflac_md5_interleaved32(const int32_t *pcm, uint64_t nsamples, uint32_t channels,
+                                                   uint32_t bps, uint8_t out_md5[16]) {
+    if ((!pcm && nsamples) || !out_md5) return fail("bnflac_md5_interleaved32: null pointer");
+    if (channels < 1 || channels > FLAC__MAX_CHANNELS || bps < 4 || bps > 32)
+        return fail("bnflac_md5_interleaved32: bad channels/bps");
+    Md5 m;
+    md5_init(m);
+    const int32_t *chan[FLAC__MAX_CHANNELS];
+    for (uint32_t c = 0; c < channels; c++) chan[c] = pcm + c;
+    md5_accumulate(m, chan, channels, nsamples, channels, (bps + 7) / 8);
+    md5_final(m, out_md5);
+    return 0;
+}
+
 extern "C" BNFLAC_API int bnflac_index_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
                                               uint64_t *d_offsets, uint32_t cap, uint32_t *d_count, void *hs) {
     if (!ctx) return fail("bnflac_index_frames: null ctx");
@@ -277,6 +292,10 @@ struct FLAC__StreamDecoder {
     unsigned fixed_block_size = 0, next_fixed_block_size = 0;
     uint64_t first_frame_offset = 0;
     bool is_seeking = false;
+    /* MD5 of the decoded PCM vs STREAMINFO md5sum (stream_decoder.c md5_checking /
+     * do_md5_checking / md5context); off unless set_md5_checking(true) before init */
+    bool md5_checking = false, do_md5 = false;
+    Md5 md5;
     uint64_t seek_target = 0;
     int seek_done = 0;
 
@@ -475,6 +494,10 @@ bool read_metadata(Dec *d) {
         if (!need_bytes(d, end / 8)) return false;
         d->bitpos_meta = end;
         d->has_stream_info = true;
+        /* an all-zero md5sum means "not computed": nothing to check against */
+        bool zero = true;
+        for (int i = 0; i < 16; i++) zero = zero && si.md5sum[i] == 0;
+        if (zero) d->do_md5 = false;
         if (d->metadata_cb && !d->is_seeking) d->metadata_cb(d, &m, d->client);
     } else {
         uint64_t end = d->bitpos_meta + (uint64_t)length * 8;
@@ -789,6 +812,9 @@ bool read_frame(Dec *d, bool *got) {
         d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
         return true;
     }
+    /* write_audio_frame_to_client_: no STREAMINFO -> no sum to compare, stop hashing */
+    if (!d->has_stream_info) d->do_md5 = false;
+    if (d->do_md5) md5_accumulate(d->md5, bufs, h.channels, h.blocksize, 1, (h.bits_per_sample + 7) / 8);
     FLAC__StreamDecoderWriteStatus ws = d->write_cb(d, &d->frame, bufs, d->client);
     if (ws != FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE && !d->ignore_write_status) return false; /* state stays READ_FRAME */
     d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
@@ -810,6 +836,8 @@ void reset_fields(Dec *d) {
     d->info.clear();
     d->pcm.clear();
     d->is_seeking = false;
+    d->do_md5 = d->md5_checking;
+    md5_init(d->md5);
 }
 
 /* file callbacks (stream_decoder.c file_*_callback_) */
@@ -907,11 +935,28 @@ BNFLAC_API FLAC__bool FLAC__stream_decoder_finish(FLAC__StreamDecoder *d) {
     if (d->state == FLAC__STREAM_DECODER_UNINITIALIZED) return 1;
     if (d->file && d->file != stdin) fclose(d->file);
     d->file = nullptr;
+    bool md5_failed = false;
+    if (d->do_md5) {
+        uint8_t sum[16];
+        md5_final(d->md5, sum);
+        md5_failed = memcmp(sum, d->stream_info.data.stream_info.md5sum, 16) != 0;
+    }
     reset_fields(d);
     for (unsigned i = 0; i < FLAC__MAX_CHANNELS; i++) d->output[i].clear();
     d->output_capacity = d->output_channels = 0;
+    d->md5_checking = false; /* set_defaults_ */
     d->state = FLAC__STREAM_DECODER_UNINITIALIZED;
-    return 1; /* MD5 checking is off by default (BirdNest never enables it) */
+    return md5_failed ? 0 : 1;
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_set_md5_checking(FLAC__StreamDecoder *d, FLAC__bool value) {
+    if (!d || d->state != FLAC__STREAM_DECODER_UNINITIALIZED) return 0;
+    d->md5_checking = value != 0;
+    return 1;
+}
+
+BNFLAC_API FLAC__bool FLAC__stream_decoder_get_md5_checking(const FLAC__StreamDecoder *d) {
+    return (d && d->md5_checking) ? 1 : 0;
 }
 
 BNFLAC_API FLAC__bool FLAC__stream_decoder_delete(FLAC__StreamDecoder *d) {
@@ -1010,6 +1055,7 @@ BNFLAC_API FLAC__bool FLAC__stream_decoder_seek_absolute(FLAC__StreamDecoder *d,
     }
     /* Walk frames from the first frame (every byte read so far is still buffered) until
      * the one holding `sample`; only that frame reaches the write callback, trimmed. */
+    d->do_md5 = false; /* a seek turns MD5 checking off (stream_decoder.c seek_absolute) */
     d->is_seeking = true;
     d->seek_target = sample;
     d->seek_done = 0;

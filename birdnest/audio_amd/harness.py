@@ -17,7 +17,10 @@ from .libflac import (LibFLAC, DecoderEofCallback, DecoderReadCallback, DecoderW
 EV_METADATA, EV_WRITE, EV_ERROR, EV_RETURN = 1, 2, 3, 4
 
 
-def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: int = -1):
+def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: int = -1, md5_check: bool = False):
+    """-> (events, pcm); with md5_check, MD5 checking is enabled before init and the
+    result is (events, pcm, finish_ok) where finish_ok is FLAC__stream_decoder_finish's
+    return (false on an MD5 mismatch)."""
     L = load()
     data = bytes(data)
     st = {"pos": 0, "eof": False, "frames": 0}
@@ -25,6 +28,10 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
     pcm_parts = []
     npcm = [0]
     dec = L.FLAC__stream_decoder_new()
+    if md5_check and not L.FLAC__stream_decoder_set_md5_checking(dec, 1):
+        L.FLAC__stream_decoder_delete(dec)
+        raise RuntimeError("set_md5_checking refused before init")
+    finish_ok = None
 
     def state():
         return int(L.FLAC__stream_decoder_get_state(dec))
@@ -98,9 +105,13 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
         else:
             ok = int(L.FLAC__stream_decoder_process_until_end_of_stream(dec))
             events.append((EV_RETURN, ok, state(), 0, 0, 0, 0, 0, 0, 0))
+        if md5_check:
+            finish_ok = bool(L.FLAC__stream_decoder_finish(dec))
     finally:
         L.FLAC__stream_decoder_delete(dec)
     pcm = np.concatenate(pcm_parts) if pcm_parts else np.zeros(0, dtype=np.int32)
+    if md5_check:
+        return events, pcm, finish_ok
     return events, pcm
 
 

@@ -120,10 +120,12 @@ DECODER_SYMBOLS = [
     "FLAC__stream_decoder_get_total_samples", "FLAC__stream_decoder_get_channels",
     "FLAC__stream_decoder_get_bits_per_sample", "FLAC__stream_decoder_get_sample_rate",
     "FLAC__stream_decoder_get_state", "FLAC__stream_decoder_reset", "FLAC__stream_decoder_init_stream",
+    "FLAC__stream_decoder_set_md5_checking", "FLAC__stream_decoder_get_md5_checking",
 ]
 BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error", "bnflac_device_count",
                  "bnflac_index_frames", "bnflac_decode_frames", "bnflac_parse_frames", "bnflac_decode_parsed",
-                 "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats"]
+                 "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats",
+                 "bnflac_md5_interleaved32"]
 
 _LIB = None
 
@@ -173,6 +175,12 @@ def load() -> ctypes.CDLL:
     L.bnflac_debug_stats.restype = ctypes.c_int
     L.bnflac_out_stride.restype = ctypes.c_uint32
     L.bnflac_out_stride.argtypes = [i, p]
+    L.FLAC__stream_decoder_set_md5_checking.restype = b
+    L.FLAC__stream_decoder_set_md5_checking.argtypes = [p, b]
+    L.FLAC__stream_decoder_get_md5_checking.restype = b
+    L.FLAC__stream_decoder_get_md5_checking.argtypes = [p]
+    L.bnflac_md5_interleaved32.restype = i
+    L.bnflac_md5_interleaved32.argtypes = [p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, p]
     _LIB = L
     return L
 
@@ -246,6 +254,14 @@ class LibFLAC:
     def FLAC__stream_decoder_reset(ctx):
         return int(LibFLAC._l().FLAC__stream_decoder_reset(ctx))
 
+    @staticmethod
+    def FLAC__stream_decoder_set_md5_checking(ctx, value):
+        return bool(LibFLAC._l().FLAC__stream_decoder_set_md5_checking(ctx, 1 if value else 0))
+
+    @staticmethod
+    def FLAC__stream_decoder_get_md5_checking(ctx):
+        return bool(LibFLAC._l().FLAC__stream_decoder_get_md5_checking(ctx))
+
 
 # ------------------------------------------------------------------ batch API
 OUT_PLANAR32, OUT_INTERLEAVED32, OUT_FLACDECODER, OUT_FILEREADER = 0, 1, 2, 3
@@ -276,6 +292,18 @@ class StreamParams(ctypes.Structure):
 
 def out_stride(fmt: int, sp: StreamParams) -> int:
     return int(load().bnflac_out_stride(fmt, ctypes.byref(sp)))
+
+
+def md5_interleaved32(pcm: np.ndarray, channels: int, bps: int) -> bytes:
+    """STREAMINFO md5sum of interleaved int32 PCM (host), libFLAC's byte convention."""
+    a = np.ascontiguousarray(pcm, dtype=np.int32).reshape(-1)
+    if a.size % channels:
+        raise ValueError("pcm size is not a multiple of channels")
+    out = (ctypes.c_uint8 * 16)()
+    rc = load().bnflac_md5_interleaved32(a.ctypes.data if a.size else None, a.size // channels, channels, bps, out)
+    if rc != 0:
+        raise RuntimeError(load().bnflac_last_error().decode())
+    return bytes(out)
 
 
 class BatchDecoder:

@@ -78,6 +78,11 @@ BNFLAC_API int FLAC__stream_decoder_init_stream(FLAC__StreamDecoder *decoder,
                                                 FLAC__StreamDecoderMetadataCallback metadata_callback,
                                                 FLAC__StreamDecoderErrorCallback error_callback,
                                                 void *client_data);
+/* libFLAC stream_decoder.h (not bound by LibFLACSharp.cs; BirdNest leaves MD5 checking
+ * off).  Only while UNINITIALIZED; finish() then returns false when the MD5 of the
+ * decoded PCM differs from STREAMINFO's non-zero md5sum.  A seek turns checking off. */
+BNFLAC_API FLAC__bool FLAC__stream_decoder_set_md5_checking(FLAC__StreamDecoder *decoder, FLAC__bool value);
+BNFLAC_API FLAC__bool FLAC__stream_decoder_get_md5_checking(const FLAC__StreamDecoder *decoder);
 
 /* ========================= Part 2: batched device-pointer API ========================= */
 
@@ -160,6 +165,12 @@ BNFLAC_API int bnflac_debug_stats(uint64_t *out16, int reset);
 
 /* Bytes of one sample frame (all channels of one sample index) in out_format. */
 BNFLAC_API uint32_t bnflac_out_stride(int out_format, const bnflac_stream_params *sp);
+
+/* Host helper: STREAMINFO md5sum of nsamples interleaved int32 sample frames (host
+ * memory, e.g. a BNFLAC_OUT_INTERLEAVED32 result copied back), hashed as libFLAC does:
+ * each sample as (bps + 7) / 8 little-endian bytes.  0 on success. */
+BNFLAC_API int bnflac_md5_interleaved32(const int32_t *pcm, uint64_t nsamples, uint32_t channels, uint32_t bps,
+                                        uint8_t out_md5[16]);
 
 #ifdef __cplusplus
 }

@@ -70,3 +70,32 @@ def test_no_gpu_fails_loudly():
         libflac.Decoder_ErrorCallback(lambda *a: None), None)
     assert rc == 3  # MEMORY_ALLOCATION_ERROR: no CPU fallback
     assert L.FLAC__stream_decoder_delete(d) == 1  # bool-declared delete returns true (SURVEY 8b hazard 1)
+
+
+@pytest.mark.parametrize("channels,bps", [(2, 16), (1, 8), (2, 24), (6, 20), (3, 32), (1, 4)])
+def test_md5_helper_matches_libflac_convention(channels, bps):
+    """bnflac_md5_interleaved32 (host MD5) vs hashlib over libFLAC's byte
+    layout (FLAC__MD5Accumulate: interleaved, (bps+7)/8 little-endian bytes per sample)."""
+    import hashlib
+
+    import numpy as np
+    rng = np.random.default_rng(channels * 100 + bps)
+    n = 3001
+    lo, hi = -(1 << (bps - 1)), (1 << (bps - 1))
+    pcm = rng.integers(lo, hi, size=n * channels, dtype=np.int64).astype(np.int32)
+    nb = (bps + 7) // 8
+    raw = pcm.astype("<i4").view(np.uint8).reshape(-1, 4)[:, :nb].tobytes()
+    assert libflac.md5_interleaved32(pcm, channels, bps) == hashlib.md5(raw).digest()
+    assert libflac.md5_interleaved32(np.zeros(0, np.int32), channels, bps) == hashlib.md5(b"").digest()
+
+
+def test_md5_checking_setter_only_while_uninitialized():
+    L = libflac.load()
+    d = L.FLAC__stream_decoder_new()
+    assert L.FLAC__stream_decoder_get_md5_checking(d) == 0  # libFLAC default: off
+    assert L.FLAC__stream_decoder_set_md5_checking(d, 1) == 1
+    assert L.FLAC__stream_decoder_get_md5_checking(d) == 1
+    assert L.FLAC__stream_decoder_set_md5_checking(d, 0) == 1
+    assert L.FLAC__stream_decoder_get_md5_checking(d) == 0
+    assert L.FLAC__stream_decoder_finish(d) == 1  # uninitialised finish: true
+    assert L.FLAC__stream_decoder_delete(d) == 1

@@ -269,6 +269,84 @@ def test_stream_api_large_c2_windows(gpu):
     assert np.array_equal(pcm, opcm)
 
 
+# ------------------------------------------------ MD5 verification
+MD5_CASES = [k for k, v in GOLD.items() if v["kind"] in ("roundtrip", "rfc")]
+
+
+@pytest.mark.parametrize("name", MD5_CASES)
+def test_md5_checking_passes_on_golden(gpu, name):
+    """set_md5_checking(true): finish() is true when the decoded PCM hashes to STREAMINFO's
+    md5sum (rfc9639_ex1's sum is the RFC's own), and checking changes no callback."""
+    from birdnest.audio_amd import harness
+    data = _read(name)
+    assert data[26:42].hex() == GOLD[name]["md5"]
+    ev, pcm = harness.run(data, driver=1)
+    ev2, pcm2, ok = harness.run(data, driver=1, md5_check=True)
+    assert ok is True
+    assert ev2 == ev and np.array_equal(pcm2, pcm)
+
+
+def test_md5_checking_detects_mismatch(gpu):
+    from birdnest.audio_amd import harness
+    data = bytearray(_read("c3_lpc12_ms_wasted"))
+    data[30] ^= 0x01  # STREAMINFO md5sum byte 4
+    ev, pcm, ok = harness.run(bytes(data), driver=0, md5_check=True)
+    assert ok is False
+    # checking off (the default): finish is true whatever the sum says
+    d = bytearray(data)
+    ev_off, _ = harness.run(bytes(d), driver=0)
+    assert ev_off == ev
+    data[26:42] = bytes(16)  # all-zero sum: nothing to check
+    assert harness.run(bytes(data), driver=0, md5_check=True)[2] is True
+
+
+def test_md5_checking_hashes_zeroed_crc_frames(gpu):
+    """A CRC-16 mismatch frame is written as silence and hashed as such (libFLAC), so the
+    stream's true sum no longer matches."""
+    from birdnest.audio_amd import harness
+    data = _read("err_crc16_mismatch")
+    ev, pcm, ok = harness.run(data, driver=1, md5_check=True)
+    assert any(e[0] == harness.EV_ERROR for e in ev)
+    si_md5 = data[26:42]
+    if si_md5 != bytes(16):
+        assert ok is False
+
+
+def test_md5_checking_off_after_seek(gpu, tmp_path):
+    """seek_absolute turns MD5 checking off: a wrong sum no longer fails finish()."""
+    import ctypes
+    torch, libflac, _ = gpu
+    L = libflac.load()
+    data = bytearray(_read("c2_lpc8"))
+    data[26] ^= 0xFF
+    path = tmp_path / "bad_md5.flac"
+    path.write_bytes(bytes(data))
+    wr = libflac.DecoderWriteCallbackWithStatus(lambda *a: 0)
+    er = libflac.Decoder_ErrorCallback(lambda *a: None)
+    md = libflac.Decoder_MetadataCallback()
+    for seek in (False, True):
+        d = L.FLAC__stream_decoder_new()
+        assert L.FLAC__stream_decoder_set_md5_checking(d, 1)
+        assert L.FLAC__stream_decoder_init_file(d, str(path).encode(), wr, md, er, None) == 0
+        assert not L.FLAC__stream_decoder_set_md5_checking(d, 0)  # refused once initialised
+        assert L.FLAC__stream_decoder_process_until_end_of_metadata(d)
+        if seek:
+            assert L.FLAC__stream_decoder_seek_absolute(d, ctypes.c_uint64(5000))
+        assert L.FLAC__stream_decoder_process_until_end_of_stream(d)
+        assert bool(L.FLAC__stream_decoder_finish(d)) is seek
+        assert L.FLAC__stream_decoder_get_md5_checking(d) == 0  # finish restores defaults
+        L.FLAC__stream_decoder_delete(d)
+
+
+def test_md5_helper_on_batch_output(gpu):
+    """Batch path: interleaved32 output hashed by bnflac_md5_interleaved32 == STREAMINFO sum."""
+    torch, libflac, _ = gpu
+    for name in ("c2_lpc8", "c5_lpc32_8ch", "mono_8bit_fixed"):
+        data = _read(name)
+        out, info, sp = _decode_batch(gpu, data, GOLD[name]["frame_offsets"], libflac.OUT_INTERLEAVED32)
+        assert libflac.md5_interleaved32(out.view("<i4"), sp.channels, sp.bps) == data[26:42], name
+
+
 # ------------------------------------------------ stereo fast path (k_decode_st)
 FL_ST, FL_REDO = 32, 64
 
