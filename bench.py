@@ -51,6 +51,7 @@ def parse_args():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads for the multi-thread CPU baseline (0: min(16, cpu count))")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-resident) measurement")
+    ap.add_argument("--no-index", action="store_true", help="skip the frame-indexer (bnflac_index_stream) timing")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--stats", action="store_true", help="report k_decode event counters (one extra step)")
     ap.add_argument("--ablate", default=None,
@@ -147,6 +148,26 @@ def pcie_inclusive(args, torch, dev, libflac, dec, data, offs, sp, p, s, pcm_byt
     return {"value": round(samples_per_batch * nb * reps / el / 1e6, 2), "unit": "MSamples/s",
             "batches": nb * reps, "bitexact": bool(ok),
             "note": "pinned host bytes -> H2D -> k_parse+k_decode -> D2H PCM, serialized on one stream"}
+
+
+def index_leg(torch, dev, libflac, dec, data, offs, sp, reps=5):
+    """bnflac_index_stream over one whole C2 stream in HBM: sync scan,
+    candidate parse, CRC-16 chain.  Wall time per call (it syncs once for the candidate
+    count).  Reported beside `value`, not part of it."""
+    n = len(data)
+    d = torch.zeros((n + 15) // 16 * 16 + 16, dtype=torch.uint8, device=dev)
+    d[:n] = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).to(dev)
+    cap = len(offs) + 16
+    o, _, _, nf = dec.index_stream(d, n, int(offs[0]), sp, cap)
+    match = nf == len(offs) and bool(np.array_equal(o[:nf].cpu().numpy(), offs))
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dec.index_stream(d, n, int(offs[0]), sp, cap)
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"ms": round(ms, 4), "GB_per_s": round(n / (ms * 1e-3) / 1e9, 2), "frames": nf, "stream_bytes": n,
+            "matches_generator_offsets": match,
+            "note": "one C2 stream: sync scan + k_parse of every candidate + CRC-16 chain (one host sync)"}
 
 
 def main():
@@ -342,6 +363,8 @@ def main():
                         "k_decode_ms": round(sum(a.elapsed_time(b) for a, b in de) / len(de), 4)})
         dec.L.bnflac_debug_set_ablate(0)
         line["ablation"] = abl
+    if rank == 0 and not args.no_index:
+        line["indexer"] = index_leg(torch, dev, libflac, dec, data, offs, sp)
     if rank == 0 and not args.no_pcie:
         line["pcie_inclusive"] = pcie_inclusive(args, torch, dev, libflac, dec, data, offs, sp, p, s,
                                                 pcm_bytes_per_batch, samples_per_batch)

@@ -1548,6 +1548,190 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
     }
 }
 
+#if BNF_TU == 0
+/* ============================================================ frame chain (8f-1)
+ * Which sync candidates are frames.  libFLAC finds the next frame where the previous one
+ * ends (read_frame_ leaves the reader after the CRC-16 footer, frame_sync_ @0x10011760
+ * looks for a sync code right there).  A frame's footer makes the CRC-16 of the whole
+ * frame zero, so without decoding anything: candidate j follows valid candidate i iff
+ * CRC-16(bytes[c_i, c_j)) == 0 and j itself has a valid header (CRC-8) and subframe walk;
+ * the first such j is taken.
+ * With P(y) = CRC-16(bytes[0, y)) and R(y) = P(y) * x^(8(N - y)) mod G (N = nbytes, x is
+ * invertible mod G), CRC-16(bytes[a, b)) * x^(8(N - b)) = R(b) + R(a), so the test is the
+ * equality of two per-candidate keys R(c).  R(c_j) is the XOR prefix over the gaps
+ * g < j of CRC-16(gap g) * x^(8(N - end of g)).  The stream's frames are then the
+ * successor chain from the first valid candidate at or after the first frame offset,
+ * found by pointer doubling (log2 n rounds) and compacted in stream order. */
+#define CHAIN_WIN (1u << 16) /* candidates looked at past a frame start for its successor */
+#define KEY_OK 0x10000u      /* key bit 16: the candidate parsed as a valid frame start */
+
+/* CRC-16 of the gap between consecutive candidates (the last one runs to nbytes), shifted
+ * to the end of the buffer: one wave per gap, 16-byte-aligned slices per lane, lane CRCs
+ * shifted to the buffer end and XOR-reduced. */
+__global__ void __launch_bounds__(256) k_gap_crc(const uint8_t *__restrict__ bytes, uint64_t nbytes,
+                                                 const uint64_t *__restrict__ cand, uint32_t ncand,
+                                                 uint32_t *__restrict__ gap_w) {
+    __shared__ uint16_t tab[8 * 256];
+    for (uint32_t i = threadIdx.x; i < 8u * 256u; i += 256u) tab[i] = (&g_crc16_tab[0][0])[i];
+    __syncthreads();
+    const lds_u16 *T = (const lds_u16 *)(lds_u32 *)tab;
+    const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (g >= ncand) return;
+    const uint64_t b0 = cand[g];
+    const uint64_t b1 = g + 1 < ncand ? cand[g + 1] : nbytes;
+    const uint64_t slice = ((b1 - b0 + 63u) / 64u + 15u) & ~15ull;
+    const uint64_t s0 = min(b1, b0 + slice * lane);
+    const uint64_t s1 = min(b1, s0 + slice);
+    uint32_t c = s0 < s1 ? crc16_shift(crc16_range(bytes, s0, s1, T), nbytes - s1) : 0u;
+    for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
+    if (lane == 0) gap_w[g] = c;
+}
+
+/* single-workgroup exclusive XOR scan of the gap words -> keys (in place), KEY_OK added */
+__global__ void __launch_bounds__(1024) k_chain_keys(uint32_t *__restrict__ v, uint32_t n,
+                                                     const bnf_frame_info *__restrict__ info) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t x = i < n ? v[i] : 0u;
+        uint32_t incl = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if ((threadIdx.x & 63) >= (unsigned)o) incl ^= y;
+        }
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 1; w < 16; w++) wsum[w] ^= wsum[w - 1];
+        __syncthreads();
+        const uint32_t wprefix = (threadIdx.x >= 64) ? wsum[(threadIdx.x >> 6) - 1] : 0u;
+        if (i < n) v[i] = (carry ^ wprefix ^ incl ^ x) | (info[i].status == BNF_ST_OK ? KEY_OK : 0u);
+        __syncthreads();
+        if (threadIdx.x == 1023) carry ^= wprefix ^ incl;
+        __syncthreads();
+    }
+}
+
+/* succ[i]: index of the candidate where frame i ends, -1 if none (or i is not valid);
+ * head: the first valid candidate at or after first_off (atomicMin; preset to INT_MAX). */
+__global__ void __launch_bounds__(256) k_chain_succ(const uint64_t *__restrict__ cand, uint32_t ncand,
+                                                    const uint32_t *__restrict__ key, uint64_t first_off,
+                                                    int32_t *__restrict__ succ, int32_t *__restrict__ head) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= ncand) return;
+    int32_t s = -1;
+    const uint32_t want = key[i];
+    if (want & KEY_OK) {
+        if (cand[i] >= first_off) atomicMin(head, (int32_t)i);
+        const uint32_t jend = (uint32_t)min((uint64_t)ncand, (uint64_t)i + 1u + CHAIN_WIN);
+        for (uint32_t j = i + 1; j < jend; j++)
+            if (key[j] == want) {
+                s = (int32_t)j;
+                break;
+            }
+    }
+    succ[i] = s;
+}
+
+/* pointer doubling: dst[i] = src[src[i]] */
+__global__ void __launch_bounds__(256) k_chain_jump(const int32_t *__restrict__ src, int32_t *__restrict__ dst,
+                                                    uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const int32_t a = src[i];
+    dst[i] = a < 0 ? -1 : src[a];
+}
+
+/* mark[jump[i]] for every marked i.  Levels are applied from the longest jump down: the
+ * marked set becomes {succ^t(head) : t < 2^levels}.  A mark set during the same launch
+ * only adds further chain members, so the in-launch races are harmless. */
+__global__ void __launch_bounds__(256) k_chain_mark(const int32_t *__restrict__ jump, uint32_t *__restrict__ mark,
+                                                    uint32_t n, const int32_t *__restrict__ head, int first) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    if (first) {
+        if ((int32_t)i == *head) mark[i] = 1u;
+        return;
+    }
+    if (mark[i]) {
+        const int32_t j = jump[i];
+        if (j >= 0) mark[j] = 1u;
+    }
+}
+
+/* write the chain in stream order: pos = exclusive scan of mark */
+__global__ void __launch_bounds__(256) k_chain_compact(const uint64_t *__restrict__ cand, uint32_t ncand,
+                                                       const bnf_frame_info *__restrict__ info,
+                                                       const uint32_t *__restrict__ mark, const uint32_t *__restrict__ pos,
+                                                       uint64_t *__restrict__ bs, uint32_t scratch_cap) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= ncand || !mark[i]) return;
+    const uint32_t p = pos[i];
+    if (p < scratch_cap) bs[p] = info[i].blocksize;
+}
+
+/* single-workgroup exclusive scan of v[0, *n) (64-bit), total in *total */
+__global__ void __launch_bounds__(1024) k_scan_u64(uint64_t *__restrict__ v, const uint32_t *__restrict__ n_ptr,
+                                                   uint32_t cap, uint64_t *__restrict__ total) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    const uint32_t n = min(*n_ptr, cap);
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const uint64_t x = i < n ? v[i] : 0ull;
+        uint64_t incl = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(incl, o);
+            if ((threadIdx.x & 63) >= (unsigned)o) incl += y;
+        }
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 1; w < 16; w++) wsum[w] += wsum[w - 1];
+        __syncthreads();
+        const uint64_t wprefix = (threadIdx.x >= 64) ? wsum[(threadIdx.x >> 6) - 1] : 0ull;
+        if (i < n) v[i] = carry + wprefix + incl - x;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += wprefix + incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+/* outputs; frames starting at or past total_samples are dropped (frame_sync_'s EOS rule,
+ * @0x100117a7): nframes = min(chain length, first such position) */
+__global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__ cand, uint32_t ncand,
+                                                    const bnf_frame_info *__restrict__ info,
+                                                    const uint32_t *__restrict__ mark, const uint32_t *__restrict__ pos,
+                                                    const uint64_t *__restrict__ out_sample, bnf_stream_params sp,
+                                                    uint64_t *__restrict__ d_offs, uint64_t *__restrict__ d_os,
+                                                    bnf_frame_info *__restrict__ d_info, uint32_t cap,
+                                                    uint32_t *__restrict__ nframes) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= ncand || !mark[i]) return;
+    const uint32_t p = pos[i];
+    if (p >= cap) return;
+    const uint64_t os = out_sample[p];
+    if (sp.has_stream_info && sp.total_samples > 0 && os >= sp.total_samples) {
+        atomicMin(nframes, p);
+        return;
+    }
+    d_offs[p] = cand[i];
+    if (d_os) d_os[p] = os;
+    if (d_info) {
+        bnf_frame_info fi = info[i];
+        fi.out_sample = os;
+        d_info[p] = fi;
+    }
+}
+#endif /* BNF_TU == 0 */
+
 #if BNF_TU == 3 || BNF_TU == 4
 /* =============================================================== k_decode_st
  * Stereo fast path: one lane per 2-channel frame (both subframes, two independent bit
@@ -2383,6 +2567,45 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
     if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
     if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
     return e;
+}
+
+/* Frame chain over ncand parsed candidates (see k_gap_crc).  Scratch (device): gap_crc,
+ * mark, pos: ncand u32 each; jump: levels * ncand i32; bs: ncand u64; small: 64 bytes.
+ * *nframes (device) receives the chain length after the EOS rule (may exceed cap). */
+hipError_t bnf_launch_chain(const uint8_t *bytes, uint64_t nbytes, const uint64_t *cand, uint32_t ncand,
+                            const bnf_frame_info *info, uint64_t first_off, bnf_stream_params sp, uint32_t *gap_crc,
+                            int32_t *jump, uint32_t levels, uint32_t *mark, uint32_t *pos, uint64_t *bs, uint8_t *small,
+                            uint64_t *d_offs, uint64_t *d_os, bnf_frame_info *d_info, uint32_t cap, uint32_t *nframes,
+                            hipStream_t s) {
+    int32_t *head = (int32_t *)small;
+    uint32_t *chain_len = (uint32_t *)(small + 8);
+    uint64_t *samples = (uint64_t *)(small + 16);
+    hipError_t e = hipMemsetAsync(head, 0x7f, 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(mark, 0, sizeof(uint32_t) * (size_t)ncand, s);
+    if (e != hipSuccess) return e;
+    const dim3 g256((ncand + 255) / 256);
+    if (ncand) {
+        hipLaunchKernelGGL(k_gap_crc, dim3((ncand + 3) / 4), dim3(256), 0, s, bytes, nbytes, cand, ncand, gap_crc);
+        hipLaunchKernelGGL(k_chain_keys, dim3(1), dim3(1024), 0, s, gap_crc, ncand, info);
+        hipLaunchKernelGGL(k_chain_succ, g256, dim3(256), 0, s, cand, ncand, gap_crc, first_off, jump, head);
+        for (uint32_t k = 0; k + 1 < levels; k++)
+            hipLaunchKernelGGL(k_chain_jump, g256, dim3(256), 0, s, jump + (size_t)k * ncand,
+                               jump + (size_t)(k + 1) * ncand, ncand);
+        hipLaunchKernelGGL(k_chain_mark, g256, dim3(256), 0, s, jump, mark, ncand, head, 1);
+        for (int k = (int)levels - 1; k >= 0; k--)
+            hipLaunchKernelGGL(k_chain_mark, g256, dim3(256), 0, s, jump + (size_t)k * ncand, mark, ncand, head, 0);
+        e = hipMemcpyAsync(pos, mark, sizeof(uint32_t) * (size_t)ncand, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, pos, ncand, chain_len);
+    hipLaunchKernelGGL(k_chain_compact, g256, dim3(256), 0, s, cand, ncand, info, mark, pos, bs, ncand);
+    hipLaunchKernelGGL(k_scan_u64, dim3(1), dim3(1024), 0, s, bs, chain_len, ncand, samples);
+    e = hipMemcpyAsync(nframes, chain_len, 4, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+    if (ncand)
+        hipLaunchKernelGGL(k_chain_emit, g256, dim3(256), 0, s, cand, ncand, info, mark, pos, bs, sp, d_offs, d_os,
+                           d_info, cap, nframes);
+    return hipGetLastError();
 }
 
 hipError_t bnf_launch_scan_u32(uint32_t *v, uint32_t n, uint32_t *total, hipStream_t s) {

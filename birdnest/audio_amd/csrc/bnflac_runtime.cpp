@@ -48,6 +48,11 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes,
                              bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
                              bnf_frame_info *info, hipStream_t s);
+hipError_t bnf_launch_chain(const uint8_t *bytes, uint64_t nbytes, const uint64_t *cand, uint32_t ncand,
+                            const bnf_frame_info *info, uint64_t first_off, bnf_stream_params sp, uint32_t *gap_crc,
+                            int32_t *jump, uint32_t levels, uint32_t *mark, uint32_t *pos, uint64_t *bs, uint8_t *small,
+                            uint64_t *d_offs, uint64_t *d_os, bnf_frame_info *d_info, uint32_t cap, uint32_t *nframes,
+                            hipStream_t s);
 }
 
 /* ------------------------------------------------------------------ errors */
@@ -123,10 +128,31 @@ extern "C" BNFLAC_API int bnflac_device_count(void) {
 }
 
 /* ----------------------------------------------------------------- context */
+struct CtxBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    bool grow(size_t n) {
+        if (n <= cap) return true;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, n) != hipSuccess) return false;
+        cap = n;
+        return true;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 struct bnflac_ctx {
     int device;
     uint32_t *d_block_counts = nullptr;
     uint32_t block_cap = 0;
+    /* bnflac_index_stream scratch */
+    CtxBuf cand, info, gap, jump, mark, pos, bs, small;
 };
 
 extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
@@ -141,6 +167,8 @@ extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
 extern "C" BNFLAC_API void bnflac_ctx_destroy(bnflac_ctx *ctx) {
     if (!ctx) return;
     if (ctx->d_block_counts) (void)hipFree(ctx->d_block_counts);
+    for (CtxBuf *b : {&ctx->cand, &ctx->info, &ctx->gap, &ctx->jump, &ctx->mark, &ctx->pos, &ctx->bs, &ctx->small})
+        b->release();
     delete ctx;
 }
 
@@ -232,6 +260,49 @@ extern "C" BNFLAC_API int bnflac_decode_frames(bnflac_ctx *ctx, const uint8_t *d
     int rc = bnflac_parse_frames(ctx, d_bytes, nbytes, d_frame_offsets, nframes, sp, d_out_sample, base_sample, d_info, hs);
     if (rc) return rc;
     return bnflac_decode_parsed(ctx, d_bytes, nbytes, nframes, sp, out_format, d_out, out_bytes, d_info, hs);
+}
+
+extern "C" BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
+                                              uint64_t first_offset, const bnflac_stream_params *sp,
+                                              uint64_t *d_frame_offsets, uint64_t *d_out_sample,
+                                              bnflac_frame_info *d_info, uint32_t cap, uint32_t *d_nframes, void *hs) {
+    if (check_args(ctx, d_bytes, nbytes, sp, "bnflac_index_stream")) return -1;
+    if (!d_frame_offsets || !d_nframes) return fail("bnflac_index_stream: null output");
+    hipStream_t s = (hipStream_t)hs;
+    /* 1. sync candidates (one host sync for their count) */
+    uint32_t ccap = (uint32_t)std::min<uint64_t>(nbytes / 1024 + 4096, 1u << 30), ncand = 0;
+    for (int attempt = 0;; attempt++) {
+        if (!ctx->cand.grow(sizeof(uint64_t) * ccap) || !ctx->small.grow(64))
+            return fail("bnflac_index_stream: out of device memory");
+        if (bnflac_index_frames(ctx, d_bytes, nbytes, (uint64_t *)ctx->cand.p, ccap, (uint32_t *)ctx->small.p, hs))
+            return -1;
+        if (hipMemcpyAsync(&ncand, ctx->small.p, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return fail("bnflac_index_stream: HIP error reading the candidate count");
+        if (ncand <= ccap) break;
+        if (attempt) return fail("bnflac_index_stream: candidate count changed");
+        ccap = ncand;
+    }
+    if (ncand >= (1u << 30)) return fail("bnflac_index_stream: too many sync candidates");
+    uint32_t levels = 1;
+    while ((1ull << levels) <= ncand) levels++;
+    const size_t n = std::max<uint32_t>(ncand, 1u);
+    if (!ctx->info.grow(sizeof(bnf_frame_info) * n) || !ctx->gap.grow(4 * n) || !ctx->jump.grow(4 * n * levels) ||
+        !ctx->mark.grow(4 * n) || !ctx->pos.grow(4 * n) || !ctx->bs.grow(8 * n))
+        return fail("bnflac_index_stream: out of device memory");
+    bnf_stream_params p;
+    memcpy(&p, sp, sizeof p);
+    /* 2. header, CRC-8 and subframe walk of every candidate */
+    hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, p, nullptr,
+                                    0, (bnf_frame_info *)ctx->info.p, s);
+    /* 3. successor chain, EOS rule, compaction */
+    if (e == hipSuccess)
+        e = bnf_launch_chain(d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, (const bnf_frame_info *)ctx->info.p,
+                             first_offset, p, (uint32_t *)ctx->gap.p, (int32_t *)ctx->jump.p, levels,
+                             (uint32_t *)ctx->mark.p, (uint32_t *)ctx->pos.p, (uint64_t *)ctx->bs.p,
+                             (uint8_t *)ctx->small.p + 16, d_frame_offsets, d_out_sample, (bnf_frame_info *)d_info, cap,
+                             d_nframes, s);
+    return e == hipSuccess ? 0 : fail(std::string("bnflac_index_stream: ") + hipGetErrorString(e));
 }
 
 /* ====================================================================== */

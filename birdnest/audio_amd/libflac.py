@@ -125,7 +125,7 @@ DECODER_SYMBOLS = [
 BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error", "bnflac_device_count",
                  "bnflac_index_frames", "bnflac_decode_frames", "bnflac_parse_frames", "bnflac_decode_parsed",
                  "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats",
-                 "bnflac_md5_interleaved32"]
+                 "bnflac_md5_interleaved32", "bnflac_index_stream"]
 
 _LIB = None
 
@@ -179,6 +179,8 @@ def load() -> ctypes.CDLL:
     L.FLAC__stream_decoder_set_md5_checking.argtypes = [p, b]
     L.FLAC__stream_decoder_get_md5_checking.restype = b
     L.FLAC__stream_decoder_get_md5_checking.argtypes = [p]
+    L.bnflac_index_stream.restype = i
+    L.bnflac_index_stream.argtypes = [p, p, ctypes.c_uint64, ctypes.c_uint64, p, p, p, p, ctypes.c_uint32, p, p]
     L.bnflac_md5_interleaved32.restype = i
     L.bnflac_md5_interleaved32.argtypes = [p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, p]
     _LIB = L
@@ -341,6 +343,25 @@ class BatchDecoder:
                                         ctypes.c_void_p(d_count.data_ptr()), self._stream(stream))
         if rc != 0:
             raise RuntimeError(self.L.bnflac_last_error().decode())
+
+    def index_stream(self, d_bytes, nbytes: int, first_offset: int, sp: StreamParams, cap: int, stream=None):
+        """Frame chain of a whole stream in HBM (bnflac_index_stream).
+        -> (d_offsets int64[cap], d_out_sample int64[cap], d_info uint8[cap*128], nframes)."""
+        import torch
+        dev = d_bytes.device
+        d_offs = torch.zeros(max(cap, 1), dtype=torch.int64, device=dev)
+        d_os = torch.zeros(max(cap, 1), dtype=torch.int64, device=dev)
+        d_info = torch.zeros(max(cap, 1) * FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+        d_n = torch.zeros(1, dtype=torch.int32, device=dev)
+        rc = self.L.bnflac_index_stream(self.ctx, ctypes.c_void_p(d_bytes.data_ptr()), nbytes, first_offset,
+                                        ctypes.byref(sp), ctypes.c_void_p(d_offs.data_ptr()),
+                                        ctypes.c_void_p(d_os.data_ptr()), ctypes.c_void_p(d_info.data_ptr()), cap,
+                                        ctypes.c_void_p(d_n.data_ptr()), self._stream(stream))
+        if rc != 0:
+            raise RuntimeError(self.L.bnflac_last_error().decode())
+        s = stream if stream is not None else torch.cuda.current_stream()
+        s.synchronize()
+        return d_offs, d_os, d_info, int(d_n.item())
 
     def decode_frames(self, d_bytes, nbytes: int, d_offsets, nframes: int, sp: StreamParams, fmt: int, d_out,
                       d_info, d_out_sample=None, base_sample: int = 0, stream=None):

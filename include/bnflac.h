@@ -131,6 +131,23 @@ BNFLAC_API int bnflac_device_count(void);
 BNFLAC_API int bnflac_index_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
                                    uint64_t *d_offsets, uint32_t cap, uint32_t *d_count, void *hip_stream);
 
+/* Frame chain resolution: the frames of a whole FLAC stream resident in
+ * d_bytes (16-byte aligned, allocation >= round_up(nbytes, 16)), in stream order, without
+ * decoding them.  Sync scan -> header, CRC-8 and subframe walk of every candidate ->
+ * successor of each valid frame = the first later valid candidate at which the CRC-16 of
+ * the bytes from the frame start is zero (the CRC-16 footer zeroes it; this is where
+ * libFLAC's frame_sync_ finds the next frame in an intact stream) -> the chain from the
+ * first valid candidate at or after first_offset (the byte after the metadata blocks).
+ * Frames at or past STREAMINFO total_samples are dropped (frame_sync_'s end-of-stream
+ * rule).  Writes d_frame_offsets, d_out_sample (running sample count; may be NULL) and,
+ * when d_info != NULL, the parsed records ready for bnflac_decode_parsed.  *d_nframes
+ * (device) = chain length (only cap entries are written).  A damaged stream ends the
+ * chain at the damage; the libFLAC stream API handles resync.  Synchronises hip_stream
+ * once (candidate count); otherwise asynchronous. */
+BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, uint64_t first_offset,
+                                   const bnflac_stream_params *sp, uint64_t *d_frame_offsets, uint64_t *d_out_sample,
+                                   bnflac_frame_info *d_info, uint32_t cap, uint32_t *d_nframes, void *hip_stream);
+
 /* Decode nframes frames starting at d_frame_offsets (byte offsets into d_bytes).
  * Output position of each frame: d_out_sample[i] if non-NULL, else the header's
  * sample number (frame number x STREAMINFO blocksize for fixed-blocksize streams) minus

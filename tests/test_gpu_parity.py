@@ -269,6 +269,105 @@ def test_stream_api_large_c2_windows(gpu):
     assert np.array_equal(pcm, opcm)
 
 
+# ---------------------------------------------- frame chain indexer
+def _first_frame_offset(data: bytes) -> int:
+    """Byte after the last metadata block (what read_metadata_ leaves the reader at)."""
+    assert data[:4] == b"fLaC"
+    p = 4
+    while True:
+        hdr = data[p]
+        p += 4 + int.from_bytes(data[p + 1:p + 4], "big")
+        if hdr & 0x80:
+            return p
+
+
+def _crc16(b: bytes) -> int:
+    c = 0
+    for x in b:
+        c ^= x << 8
+        for _ in range(8):
+            c = ((c << 1) ^ 0x8005) & 0xFFFF if c & 0x8000 else (c << 1) & 0xFFFF
+    return c
+
+
+def _index(gpu, data: bytes, sp=None, first=None, cap=None):
+    torch, libflac, dec = gpu
+    sp = sp or _stream_params(libflac, data)
+    n = len(data)
+    d_bytes = torch.zeros((n + 15) // 16 * 16 + 16, dtype=torch.uint8, device="cuda:0")
+    d_bytes[:n] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda:0")
+    first = _first_frame_offset(data) if first is None else first
+    cap = cap or (n // 16 + 16)
+    offs, os_, info, nf = dec.index_stream(d_bytes, n, first, sp, cap)
+    return d_bytes, sp, offs, os_, info, nf
+
+
+@pytest.mark.parametrize("name", [k for k, v in GOLD.items() if v["kind"] == "roundtrip"])
+def test_index_stream_golden(gpu, name):
+    """Chain == the generator's frame offsets; the records it returns decode bit-exactly."""
+    torch, libflac, dec = gpu
+    g = GOLD[name]
+    data = _read(name)
+    d_bytes, sp, offs, os_, info, nf = _index(gpu, data)
+    assert nf == len(g["frame_offsets"])
+    assert offs[:nf].cpu().tolist() == list(g["frame_offsets"])
+    rec = libflac.info_array(info[: nf * libflac.FRAME_INFO_BYTES].cpu().numpy())
+    bs = rec["blocksize"].astype(np.int64)
+    assert os_[:nf].cpu().tolist() == np.concatenate([[0], np.cumsum(bs)[:-1]]).tolist()
+    assert int(bs.sum()) == sp.total_samples
+    d_out = torch.zeros(sp.total_samples * sp.channels * 4 + 64, dtype=torch.uint8, device="cuda:0")
+    dec.decode_parsed(d_bytes, len(data), nf, sp, libflac.OUT_INTERLEAVED32, d_out, info)
+    torch.cuda.synchronize()
+    pcm = d_out[: sp.total_samples * sp.channels * 4].cpu().numpy().view("<i4").reshape(-1, sp.channels)
+    assert _sha(pcm) == g["pcm_sha256"]
+
+
+@pytest.mark.parametrize("cfg,kw", [("C2", {}), ("C4", {"nframes": 600}), ("C5", {"nframes": 40}),
+                                    ("C3", {"nframes": 64})])
+def test_index_stream_synth_configs(gpu, cfg, kw):
+    from birdnest.audio_amd import synth
+    torch, libflac, dec = gpu
+    s = synth.encode(synth.config(cfg, **kw))
+    data = s.data.tobytes()
+    d_bytes, sp, offs, os_, info, nf = _index(gpu, data)
+    assert nf == len(s.frame_offsets)
+    assert np.array_equal(offs[:nf].cpu().numpy(), s.frame_offsets.astype(np.int64))
+    # trailing junk (an ID3v1-style tag holding a sync code) changes nothing
+    tail = b"TAG" + b"\xff\xf8\xc9\x18" + bytes(range(121))
+    _, _, offs2, _, _, nf2 = _index(gpu, data + tail)
+    assert nf2 == nf and torch.equal(offs2[:nf], offs[:nf])
+
+
+def test_index_stream_eos_rule_and_head(gpu):
+    torch, libflac, dec = gpu
+    g = GOLD["c4_mixed_varbs"]
+    data = _read("c4_mixed_varbs")
+    sp = _stream_params(libflac, data)
+    # STREAMINFO total_samples ending inside frame k: frames from k+1 on are past the end
+    _, _, offs, os_, info, nf = _index(gpu, data)
+    os_ = os_[:nf].cpu().numpy()
+    k = nf // 2
+    sp2 = libflac.StreamParams(1, sp.min_blocksize, sp.max_blocksize, sp.sample_rate, sp.channels, sp.bps,
+                               int(os_[k]) + 1)
+    _, _, _, _, _, nf2 = _index(gpu, data, sp=sp2)
+    assert nf2 == k + 1
+    # a first_offset inside frame 0 starts the chain at the next frame
+    _, _, offs3, _, _, nf3 = _index(gpu, data, first=g["frame_offsets"][0] + 1)
+    assert nf3 == nf - 1 and offs3[0].item() == g["frame_offsets"][1]
+
+
+def test_index_stream_stops_at_damage(gpu):
+    """A frame whose bytes fail CRC-16 has no successor: the chain ends with it."""
+    from birdnest.audio_amd import synth
+    s = synth.encode(synth.config("C2", nframes=12))
+    d = bytearray(s.data.tobytes())
+    o = [int(x) for x in s.frame_offsets]
+    d[o[6] - 10] ^= 0x10  # inside the last subframe: the header and the k_parse walk stay valid
+    assert _crc16(bytes(d[o[5]:o[6]])) != 0
+    _, _, offs, _, _, nf = _index(gpu, bytes(d))
+    assert nf == 6 and offs[:nf].cpu().tolist() == o[:6]
+
+
 # ------------------------------------------------ MD5 verification (SURVEY.md 8f-3)
 MD5_CASES = [k for k, v in GOLD.items() if v["kind"] in ("roundtrip", "rfc")]
 
