@@ -40,9 +40,9 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batches", type=int, default=192,
+    ap.add_argument("--batches", type=int, default=576,
                     help="C2 batches (x1024 frames) decoded per step; 192 = one k_decode_st wave (64 frames) "
-                         "per resident slot (256 CUs x 12 waves)")
+                         "per resident slot (256 CUs x 12 waves), 576 = three such rounds (DESIGN.md section 5)")
     ap.add_argument("--frames", type=int, default=1024, help="frames per batch (BASELINE C2: 1024)")
     ap.add_argument("--groups", type=int, default=1,
                     help="pipeline groups: k_parse of group g+1 overlaps k_decode of group g (1 = serial)")
@@ -199,11 +199,10 @@ def main():
 
     # B distinct copies of the batch in HBM (4-byte aligned), one output region each
     copy_len = (len(data) + 255) // 256 * 256
-    host = np.zeros(copy_len * B + 64, dtype=np.uint8)
-    src = np.frombuffer(data, dtype=np.uint8)
-    for b in range(B):
-        host[b * copy_len: b * copy_len + len(data)] = src
-    d_bytes = torch.from_numpy(host).to(dev)
+    one = np.zeros(copy_len, dtype=np.uint8)
+    one[:len(data)] = np.frombuffer(data, dtype=np.uint8)
+    d_bytes = torch.zeros(copy_len * B + 64, dtype=torch.uint8, device=dev)
+    d_bytes[:copy_len * B].view(B, copy_len).copy_(torch.from_numpy(one).to(dev).unsqueeze(0).expand(B, copy_len))
     nbytes_total = copy_len * B
     d_offs = torch.from_numpy(np.concatenate([offs + b * copy_len for b in range(B)])).to(dev)
     nframes = args.frames * B

@@ -1739,7 +1739,8 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  * @0x100118c0 and below) and the same PCM layouts (A15/A17), but:
  *   - the two channels' Rice + predictor chains interleave in one lane (ILP 2);
  *   - decorrelation (@0x10011a37-0x10011adb) and the PCM pack happen in registers, so
- *     there is no row buffer in LDS (LDS = the two bitstream rings, 16 KB per wave);
+ *     there is no row buffer in LDS (LDS = the two bitstream rings, 8 KB per wave, and a
+ *     4 KB tile that turns each frame's chunk of PCM into one 64-byte store run);
  *   - FIXED (@0x10003810), LPC MMX-16 and LPC ia32 restores share one predictor: eight
  *     v_mad_i32_i24 over the raw history.  That is exact while every history value fits
  *     the path's operand range (16 bits: MMX packssdw/pmaddwd see the sample itself; 24
