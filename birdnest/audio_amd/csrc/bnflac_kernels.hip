@@ -1741,11 +1741,12 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  *   - decorrelation (@0x10011a37-0x10011adb) and the PCM pack happen in registers, so
  *     there is no row buffer in LDS (LDS = the two bitstream rings, 8 KB per wave, and a
  *     4 KB tile that turns each frame's chunk of PCM into one 64-byte store run);
- *   - FIXED (@0x10003810), LPC MMX-16 and LPC ia32 restores share one predictor: eight
- *     v_mad_i32_i24 over the raw history.  That is exact while every history value fits
- *     the path's operand range (16 bits: MMX packssdw/pmaddwd see the sample itself; 24
- *     bits: the 24x24 multiply is the exact low 32 bits of the ia32 imul).  Each channel
- *     tracks its sample range; a frame that leaves it is handed back.
+ *   - FIXED (@0x10003810), LPC MMX-16 and LPC ia32 restores share one predictor: four
+ *     v_dot2_i32_i16 over the history kept as packed 16-bit sample pairs (the pmaddwd
+ *     shape).  That is exact while every sample fits 16 bits (coefficients always do:
+ *     qlp precision <= 15): the products are exact and the sums wrap mod 2^32 like the
+ *     MMX paddd, the ia32 imul/add and the FIXED int arithmetic.  Each channel tracks its
+ *     sample range; a frame that leaves int16 is handed back.
  * Frames it declines (VERBATIM/CONSTANT/64-bit-path subframes, errors, truncation, CRC
  * mismatch, out-of-range samples, unsupported layouts) get BNF_FL_REDO and are decoded
  * again, exactly, by k_decode<8>, which runs after it on the same stream. */
@@ -1754,13 +1755,21 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
 
 struct StCh {
     BR b;
-    int32_t c[8], h[8]; /* predictor coefficients (0 past the order) and history ring */
+    uint32_t cp[4]; /* coefficient pairs (c[2k] | c[2k+1] << 16, 0 past the order) */
+    uint32_t q[8];  /* history: q[m & 7] = s_m | s_(m-1) << 16 (16-bit halves) */
     int32_t sh;         /* effective shift of the libFLAC path */
     uint32_t k, km, k1, k32; /* Rice parameter, 31 - k, k + 1, 32 - k */
     uint32_t esc, left, pidx, nparts, psamples, plen, pesc, porder, order;
     uint32_t wasted;
     int32_t lim, mx, mn; /* operand range of the path, sample range seen */
 };
+
+/* lo | hi << 16 from the low halves */
+DEV uint32_t st_pk(int32_t lo, int32_t hi) { return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u); }
+typedef short st_s2 __attribute__((ext_vector_type(2)));
+DEV int32_t st_d2(uint32_t a, uint32_t b, int32_t acc) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(st_s2, a), __builtin_bit_cast(st_s2, b), acc, false);
+}
 
 /* subframe header -> fast-path state; false: hand the frame back */
 DEV bool st_setup(StCh &z, uint32_t bps, uint32_t bs, uint64_t limit) {
@@ -1770,30 +1779,34 @@ DEV bool st_setup(StCh &z, uint32_t bps, uint32_t bs, uint64_t limit) {
     if (st != BNF_ST_OK) return false;
     if (h.type != T_FIXED && h.type != T_LPC) return false;
     if (h.type == T_LPC && (h.order > 8 || h.path == P_WIDE)) return false;
-    if (h.bps > 24) return false;
+    if (h.bps > 17) return false; /* samples cannot stay within int16 */
+    int32_t c[8], w[8];
+    bool in16 = true;
 #pragma unroll
     for (int t = 0; t < 8; t++) {
-        z.c[t] = 0;
-        z.h[t] = ((uint32_t)t < h.order) ? warm[t] : 0;
+        c[t] = 0;
+        w[t] = ((uint32_t)t < h.order) ? warm[t] : 0;
+        in16 = in16 && w[t] >= -32768 && w[t] <= 32767;
     }
+    if (!in16) return false;
     z.sh = 0;
-    z.lim = 0x7FFFFF;
+    z.lim = 0x7FFF;
     if (h.type == T_LPC) {
 #pragma unroll
-        for (int t = 0; t < 8; t++) z.c[t] = ((uint32_t)t < h.order) ? coef[t] : 0;
-        if (h.path == P_MMX16) {
-            z.sh = ((uint32_t)h.shift >= 32u) ? 31 : h.shift;
-            z.lim = 0x7FFF;
-        } else {
-            z.sh = h.shift & 31;
-        }
+        for (int t = 0; t < 8; t++) c[t] = ((uint32_t)t < h.order) ? coef[t] : 0;
+        if (h.path == P_MMX16) z.sh = ((uint32_t)h.shift >= 32u) ? 31 : h.shift;
+        else z.sh = h.shift & 31;
     } else { /* FIXED order o as LPC: 1 | 2,-1 | 3,-3,1 | 4,-6,4,-1 (32-bit wrap, shift 0) */
         const uint32_t o = h.order;
-        z.c[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
-        z.c[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
-        z.c[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
-        z.c[3] = o == 4 ? -1 : 0;
+        c[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
+        c[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
+        c[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
+        c[3] = o == 4 ? -1 : 0;
     }
+#pragma unroll
+    for (int k = 0; k < 4; k++) z.cp[k] = st_pk(c[2 * k], c[2 * k + 1]);
+#pragma unroll
+    for (int t = 0; t < 8; t++) z.q[t] = st_pk(w[t], t ? w[t - 1] : 0);
     z.order = h.order;
     z.wasted = h.wasted;
     z.porder = h.porder;
@@ -1888,69 +1901,31 @@ DEV int32_t st_next(StCh &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
     return st_rice(z, limit, trunc, nst);
 }
 
-/* sum_j c[j] * h[i-1-j] (32-bit wrap, 24x24-bit products) for both channels, interleaved
- * in one asm block (no hazard padding between the dependent multiply-adds) */
+/* pred(n) = sum_j c[j] * s_(n-1-j) for sample n = I (mod 8), both channels: four dot2 over
+ * the pairs q[n-1], q[n-3], q[n-5], q[n-7] */
 template <int I>
 DEV void st_dot2(const StCh &a, const StCh &b, int32_t &pa, int32_t &pb) {
-#define H_(z, j) z.h[(I + 7 - (j)) & 7]
-    asm("v_mul_i32_i24 %0, %2, %18\n\t"
-        "v_mul_i32_i24 %1, %10, %26\n\t"
-        "v_mad_i32_i24 %0, %3, %19, %0\n\t"
-        "v_mad_i32_i24 %1, %11, %27, %1\n\t"
-        "v_mad_i32_i24 %0, %4, %20, %0\n\t"
-        "v_mad_i32_i24 %1, %12, %28, %1\n\t"
-        "v_mad_i32_i24 %0, %5, %21, %0\n\t"
-        "v_mad_i32_i24 %1, %13, %29, %1\n\t"
-        "v_mad_i32_i24 %0, %6, %22, %0\n\t"
-        "v_mad_i32_i24 %1, %14, %30, %1\n\t"
-        "v_mad_i32_i24 %0, %7, %23, %0\n\t"
-        "v_mad_i32_i24 %1, %15, %31, %1\n\t"
-        "v_mad_i32_i24 %0, %8, %24, %0\n\t"
-        "v_mad_i32_i24 %1, %16, %32, %1\n\t"
-        "v_mad_i32_i24 %0, %9, %25, %0\n\t"
-        "v_mad_i32_i24 %1, %17, %33, %1"
-        : "=&v"(pa), "=&v"(pb)
-        : "v"(a.c[0]), "v"(a.c[1]), "v"(a.c[2]), "v"(a.c[3]), "v"(a.c[4]), "v"(a.c[5]), "v"(a.c[6]), "v"(a.c[7]),
-          "v"(b.c[0]), "v"(b.c[1]), "v"(b.c[2]), "v"(b.c[3]), "v"(b.c[4]), "v"(b.c[5]), "v"(b.c[6]), "v"(b.c[7]),
-          "v"(H_(a, 0)), "v"(H_(a, 1)), "v"(H_(a, 2)), "v"(H_(a, 3)), "v"(H_(a, 4)), "v"(H_(a, 5)), "v"(H_(a, 6)), "v"(H_(a, 7)),
-          "v"(H_(b, 0)), "v"(H_(b, 1)), "v"(H_(b, 2)), "v"(H_(b, 3)), "v"(H_(b, 4)), "v"(H_(b, 5)), "v"(H_(b, 6)), "v"(H_(b, 7)));
-#undef H_
+#define Q_(z, j) z.q[(I + 8 - (j)) & 7]
+    pa = st_d2(a.cp[3], Q_(a, 7), st_d2(a.cp[2], Q_(a, 5), st_d2(a.cp[1], Q_(a, 3), st_d2(a.cp[0], Q_(a, 1), 0))));
+    pb = st_d2(b.cp[3], Q_(b, 7), st_d2(b.cp[2], Q_(b, 5), st_d2(b.cp[1], Q_(b, 3), st_d2(b.cp[0], Q_(b, 1), 0))));
+#undef Q_
 }
 
-/* The seven older taps of the NEXT sample's prediction, sum_{j=1..7} c[j] * h[T-j], from
- * the history as it stands at step T (both channels interleaved): off the critical path,
- * so only c[0] * s_T remains between consecutive samples (st_fin2). */
+/* The older taps of the NEXT sample's prediction (n = T + 1): pairs q[T-1], q[T-3], q[T-5],
+ * all known at step T, so only the newest pair's dot2 remains between consecutive samples
+ * (st_fin2). */
 template <int T>
 DEV void st_pre2(const StCh &a, const StCh &b, int32_t &pa, int32_t &pb) {
-#define P_(z, j) z.h[(T + 8 - (j)) & 7]
-    asm("v_mul_i32_i24 %0, %2, %16\n\t"
-        "v_mul_i32_i24 %1, %9, %23\n\t"
-        "v_mad_i32_i24 %0, %3, %17, %0\n\t"
-        "v_mad_i32_i24 %1, %10, %24, %1\n\t"
-        "v_mad_i32_i24 %0, %4, %18, %0\n\t"
-        "v_mad_i32_i24 %1, %11, %25, %1\n\t"
-        "v_mad_i32_i24 %0, %5, %19, %0\n\t"
-        "v_mad_i32_i24 %1, %12, %26, %1\n\t"
-        "v_mad_i32_i24 %0, %6, %20, %0\n\t"
-        "v_mad_i32_i24 %1, %13, %27, %1\n\t"
-        "v_mad_i32_i24 %0, %7, %21, %0\n\t"
-        "v_mad_i32_i24 %1, %14, %28, %1\n\t"
-        "v_mad_i32_i24 %0, %8, %22, %0\n\t"
-        "v_mad_i32_i24 %1, %15, %29, %1"
-        : "=&v"(pa), "=&v"(pb)
-        : "v"(a.c[1]), "v"(a.c[2]), "v"(a.c[3]), "v"(a.c[4]), "v"(a.c[5]), "v"(a.c[6]), "v"(a.c[7]),
-          "v"(b.c[1]), "v"(b.c[2]), "v"(b.c[3]), "v"(b.c[4]), "v"(b.c[5]), "v"(b.c[6]), "v"(b.c[7]),
-          "v"(P_(a, 1)), "v"(P_(a, 2)), "v"(P_(a, 3)), "v"(P_(a, 4)), "v"(P_(a, 5)), "v"(P_(a, 6)), "v"(P_(a, 7)),
-          "v"(P_(b, 1)), "v"(P_(b, 2)), "v"(P_(b, 3)), "v"(P_(b, 4)), "v"(P_(b, 5)), "v"(P_(b, 6)), "v"(P_(b, 7)));
+#define P_(z, j) z.q[(T + 8 - (j)) & 7]
+    pa = st_d2(a.cp[3], P_(a, 6), st_d2(a.cp[2], P_(a, 4), st_d2(a.cp[1], P_(a, 2), 0)));
+    pb = st_d2(b.cp[3], P_(b, 6), st_d2(b.cp[2], P_(b, 4), st_d2(b.cp[1], P_(b, 2), 0)));
 #undef P_
 }
-/* pred = c[0] * h + pre for both channels (the critical-path tap) */
-DEV void st_fin2(const StCh &a, const StCh &b, int32_t ha, int32_t hb, int32_t prea, int32_t preb, int32_t &pa,
+/* pred = dot2(cp[0], q[n-1]) + pre for both channels (the critical-path pair) */
+DEV void st_fin2(const StCh &a, const StCh &b, uint32_t qa, uint32_t qb, int32_t prea, int32_t preb, int32_t &pa,
                  int32_t &pb) {
-    asm("v_mad_i32_i24 %0, %2, %4, %6\n\t"
-        "v_mad_i32_i24 %1, %3, %5, %7"
-        : "=&v"(pa), "=&v"(pb)
-        : "v"(a.c[0]), "v"(b.c[0]), "v"(ha), "v"(hb), "v"(prea), "v"(preb));
+    pa = st_d2(a.cp[0], qa, prea);
+    pb = st_d2(b.cp[0], qb, preb);
 }
 
 DEV void st_range(StCh &z, int32_t s0, int32_t s1) {
@@ -2118,7 +2093,7 @@ DEV void st_fused_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
     constexpr uint32_t spg = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u;
     const uint32_t nqt = nq + ((!STG && T >= 4 && store) ? spg : 0u); /* + this group's direct store */
     int32_t p0, p1, n0, n1;
-    st_fin2(z0, z1, z0.h[(T + 7) & 7], z1.h[(T + 7) & 7], pre0, pre1, p0, p1); /* this sample's prediction */
+    st_fin2(z0, z1, z0.q[(T + 7) & 7], z1.q[(T + 7) & 7], pre0, pre1, p0, p1); /* this sample's prediction */
     st_pre2<T>(z0, z1, n0, n1);                                                /* the next one's older taps */
     pre0 = n0;
     pre1 = n1;
@@ -2142,11 +2117,11 @@ DEV void st_fused_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
     const int32_t s0 = (int32_t)(((u0 >> 1) ^ (0u - (u0 & 1u))) + (uint32_t)(p0 >> z0.sh));
     const int32_t s1 = (int32_t)(((u1 >> 1) ^ (0u - (u1 & 1u))) + (uint32_t)(p1 >> z1.sh));
     if (T & 1) {
-        st_range(z0, z0.h[(T + 7) & 7], s0);
-        st_range(z1, z1.h[(T + 7) & 7], s1);
+        st_range(z0, L[(T + 3) & 3], s0);
+        st_range(z1, R[(T + 3) & 3], s1);
     }
-    z0.h[T] = s0;
-    z1.h[T] = s1;
+    z0.q[T] = __builtin_amdgcn_perm(z0.q[(T + 7) & 7], (uint32_t)s0, 0x05040100u);
+    z1.q[T] = __builtin_amdgcn_perm(z1.q[(T + 7) & 7], (uint32_t)s1, 0x05040100u);
     L[T & 3] = s0;
     R[T & 3] = s1;
     if ((T & 3) == 3) {
@@ -2181,14 +2156,14 @@ DEV bool st_gen_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint6
     if (v) {
         int32_t p0, p1;
         st_dot2<T>(z0, z1, p0, p1);
-        if (n < z0.order) s0 = z0.h[T];
+        if (n < z0.order) s0 = (int32_t)(int16_t)z0.q[T];
         else s0 = (int32_t)((uint32_t)st_next(z0, limit, trunc, nst) + (uint32_t)(p0 >> z0.sh));
-        if (n < z1.order) s1 = z1.h[T];
+        if (n < z1.order) s1 = (int32_t)(int16_t)z1.q[T];
         else s1 = (int32_t)((uint32_t)st_next(z1, limit, trunc, nst) + (uint32_t)(p1 >> z1.sh));
         st_range(z0, s0, s0);
         st_range(z1, s1, s1);
-        z0.h[T] = s0;
-        z1.h[T] = s1;
+        z0.q[T] = __builtin_amdgcn_perm(z0.q[(T + 7) & 7], (uint32_t)s0, 0x05040100u);
+        z1.q[T] = __builtin_amdgcn_perm(z1.q[(T + 7) & 7], (uint32_t)s1, 0x05040100u);
     }
     L[T & 3] = (int32_t)((uint32_t)s0 << z0.wasted);
     R[T & 3] = (int32_t)((uint32_t)s1 << z1.wasted);
