@@ -1751,7 +1751,7 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  * mismatch, out-of-range samples, unsupported layouts) get BNF_FL_REDO and are decoded
  * again, exactly, by k_decode<8>, which runs after it on the same stream. */
 #define ST_CHK 16 /* samples per chunk (one 64-byte FLACDecoder run per frame) */
-#define ST_RD 4  /* 16-byte ring slots per lane and channel */
+#define ST_RD 8  /* 16-byte ring slots per lane and channel: two 64-byte groups */
 
 struct StCh {
     BR b;
@@ -1986,19 +1986,29 @@ DEV bool st_emit4(uint8_t *dst, uint32_t n, uint32_t nv, bool al, uint32_t bs, c
     return true;
 }
 
-/* 1-deep ring pipeline, 16-byte granular: every lane keeps its ring full -- the blocks from
- * its cursor's block up to 8 ahead -- so after the next refill's wait ~5 blocks (~20 words)
- * are landed ahead of each cursor, more than a chunk consumes at CD bit rates.  One exec-
- * masked LDS-DMA per ring slot that some lane needs.  Whole wave. */
+/* 1-deep ring pipeline in 64-byte groups: the ring holds the cursor's group and the next
+ * one; once the cursor has entered the newer of the two, the older group's slots take the
+ * group after it (four 16-byte LDS-DMAs into one half cache line).  Fetching whole groups
+ * rather than every free block keeps a cursor's refills to one per 64 bytes consumed: a
+ * cursor's line does not survive in L2 between chunks (64 x 2 cursors per wave), so each
+ * refill costs a line fetch from the fabric.  A group fetched now lands before the next
+ * refill's wait; the cursor needs it only after the ~64 bytes of the current group.
+ * Whole wave: exec-masked, and only the slot groups some lane needs are issued. */
 DEV void st_refill_issue(BR &b, bool want) {
-    const uint32_t need = b.wi >> 2; /* block holding the cursor's next word */
-    const uint32_t lo = max(b.iend, need), hi = need + ST_RD;
+    const uint32_t cg = (b.wi >> 2) & ~3u; /* first block of the cursor's group */
+    const bool go = want && b.iend == cg + 4u;
+    const uint32_t h = b.iend & 4u; /* the free group's slots: 0-3 or 4-7 */
 #pragma unroll
-    for (int s = 0; s < ST_RD; s++) {
-        const uint32_t j = lo + (((uint32_t)s - lo) & (ST_RD - 1u));
-        if (want && j < hi) dma_block(b, j, (uint32_t)s);
+    for (int g = 0; g < 2; g++) {
+        const bool gg = go && h == 4u * (uint32_t)g;
+        if (__any(gg)) {
+            if (gg) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) dma_block(b, b.iend + (uint32_t)k, 4u * (uint32_t)g + (uint32_t)k);
+            }
+        }
     }
-    if (want) b.iend = max(b.iend, hi);
+    if (go) b.iend += 4u;
 }
 
 /* CRC-16 of [b0, b1) with two 64-byte loads in flight (tables in LDS) */
@@ -2032,9 +2042,9 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
 
 /* Fused-path cursor (4-slot ring).  ra is the LDS byte offset of ring word wi inside the
  * channel's ring: bits 2-3 word in block, 4-9 lane, 10-11 slot.  Moving it one word on is
- * ((ra | 0x3F3) + c) & 0xC0C | lane bits: the ones in bits 0-1 turn +c into +4, the ones in
+ * ((ra | 0x3F3) + c) & 0x1C0C | lane bits: the ones in bits 0-1 turn +c into +4, the ones in
  * bits 4-9 carry a block wrap into the slot. */
-DEV uint32_t st_ra(uint32_t wi, uint32_t lane) { return ((wi & 3u) << 2) | (lane << 4) | (((wi >> 2) & 3u) << 10); }
+DEV uint32_t st_ra(uint32_t wi, uint32_t lane) { return ((wi & 3u) << 2) | (lane << 4) | (((wi >> 2) & 7u) << 10); }
 /* Advance by n <= 32 bits without the landing check: s - n borrows exactly when the window
  * moves on a word, and that borrow steps wi and ra (v_sub_co / v_addc). */
 DEV void st_adv_nc(BR &b, uint32_t n, uint32_t laneb) {
@@ -2044,7 +2054,7 @@ DEV void st_adv_nc(BR &b, uint32_t n, uint32_t laneb) {
     b.hi = c ? b.lo : b.hi;
     b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
     b.wi += (uint32_t)c;
-    b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0xC0Cu) | laneb;
+    b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x1C0Cu) | laneb;
 }
 DEV void st_next_word(BR &b) { b.nx = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + b.ra); }
 DEV void st_resync(BR &b, uint32_t lane) { /* after generic-reader moves: ra, vlim from wi, vendw */
@@ -2178,15 +2188,18 @@ DEV bool st_gen_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint6
 }
 
 template <int FMT>
-__global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict__ words, uint64_t nbytes,
+__global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict__ words, uint64_t nbytes,
                                                      uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                      uint8_t *__restrict__ out, uint64_t out_bytes,
                                                      bnf_frame_info *__restrict__ info, uint32_t ablate) {
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t ST_SPG = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u; /* stores per 4 samples */
-    __shared__ uint32_t ring[2 * ST_RD * RING_LANE_DW]; /* 8 KB: both channels' bitstream rings */
+    __shared__ uint32_t ring[2 * ST_RD * RING_LANE_DW]; /* 16 KB: both channels' bitstream rings */
     __shared__ uint32_t stg_tile[64 * 16];              /* 4 KB: one 64-byte PCM run per frame */
-    __shared__ uint64_t fdst[64];                       /* this chunk's run address per frame (0: none) */
+#ifdef BNF_ST_PAD
+    __shared__ uint32_t occ_pad[BNF_ST_PAD]; /* experiment: LDS padding to cap waves per CU */
+    if (ablate == 0xDEADu) occ_pad[threadIdx.x] = 1u;
+#endif
     const uint32_t lane = threadIdx.x;
     const uint32_t f = blockIdx.x * 64u + lane;
     const uint64_t limit = nbytes * 8u;
@@ -2216,6 +2229,9 @@ __global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict_
     br_init(z1.b, words, nbytes, ring1, lane, ST_RD);
     z0.b.stats = z1.b.stats = (ablate & 0x100u) != 0;
     STAT(z0.b.stats, 5);
+    const bool tmon = z0.b.stats;
+    const uint64_t t_start = tnow(tmon);
+    uint64_t tm_dec = 0, tm_ref = 0, tm_pack = 0;
     if (ok) {
         const uint64_t fbit = fi.frame_off * 8u;
         br_seek(z0.b, fbit + fi.sub_start[0]);
@@ -2240,7 +2256,9 @@ __global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict_
     uint32_t trunc = 0;
     wait_vm(); /* setup loads done: the store count starts from zero */
     uint32_t nst = 0; /* vector-memory ops (PCM stores) issued by this wave since the last refill's DMAs */
+    const uint64_t t_loop = tnow(tmon);
     for (uint32_t kc = 0; kc < nchunks; kc++) {
+        const uint64_t ta = tnow(tmon);
         const uint32_t n0 = kc * ST_CHK;
         const bool valid = ok && n0 < bs;
         bool fast = valid && n0 >= 8u && n0 + ST_CHK <= bs && !(ablate & 12u);
@@ -2271,7 +2289,7 @@ __global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict_
                 z1.left -= ST_CHK;
             }
             if (!STG && !(ablate & 2u) && any_lane(valid)) nst += (ST_CHK / 4) * ST_SPG;
-            if (STG) lds_st64((const void *)&fdst[lane], (valid && !(ablate & 2u)) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull);
+
         } else {
             STAT(z0.b.stats, 1);
 #pragma unroll 1
@@ -2290,6 +2308,8 @@ __global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict_
 #undef GSTEP
             }
         }
+        const uint64_t tb = tnow(tmon);
+        tm_dec += tb - ta;
         /* refill before the flush: wait for the previous refill's DMAs (every store since
          * stays in flight), then issue the next blocks; the flush's stores are younger */
         {
@@ -2301,14 +2321,18 @@ __global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict_
             st_refill_issue(z1.b, want);
             nst = 0;
         }
+        const uint64_t tc = tnow(tmon);
+        tm_ref += tc - tb;
         if (STG && fused) { /* flush: 4 lanes per frame, one 64-byte run each, 16 frames per store */
+            const uint64_t run = (valid && !(ablate & 2u)) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull;
             lds_sync();
             uint64_t a[4];
             u32x4 v[4];
 #pragma unroll
             for (uint32_t r = 0; r < 4; r++) {
                 const uint32_t fr = 16u * r + (lane >> 2);
-                a[r] = lds_ld64((const void *)&fdst[fr]);
+                a[r] = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(run >> 32), (int)fr) << 32) |
+                       (uint32_t)__shfl((int)(uint32_t)run, (int)fr);
                 v[r] = lds_ld128((const void *)((lds_u32 *)stg_tile + fr * 16u + 4u * ((fl_unit + (fr >> 2)) & 3u)));
             }
             lds_sync(); /* reads landed; the next chunk's staging writes come after them */
@@ -2318,7 +2342,9 @@ __global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict_
                 if (any_lane(a[r] != 0)) nst += 1u;
             }
         }
+        tm_pack += tnow(tmon) - tc;
     }
+    const uint64_t t_loopend = tnow(tmon);
 
     /* ---- end of the last subframe, zero padding, CRC-16 (read_frame_ tail) */
     uint32_t crc_read = 0;
@@ -2356,6 +2382,14 @@ __global__ void __launch_bounds__(64, 3) k_decode_st(const uint32_t *__restrict_
         info[f].crc_ok = 1u;
     } else if (mine) {
         info[f].flags = fi.flags | BNF_FL_REDO;
+    }
+    if (tmon && lane == 0) {
+        const uint64_t t_end = tnow(tmon);
+        atomicAdd(&g_stats[8], (unsigned long long)(t_loop - t_start));
+        atomicAdd(&g_stats[9], (unsigned long long)tm_dec);
+        atomicAdd(&g_stats[10], (unsigned long long)tm_ref);
+        atomicAdd(&g_stats[11], (unsigned long long)tm_pack);
+        atomicAdd(&g_stats[12], (unsigned long long)(t_end - t_loopend));
     }
 }
 #endif /* BNF_TU == 3 || BNF_TU == 4 */
