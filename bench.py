@@ -40,9 +40,9 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batches", type=int, default=576,
-                    help="C2 batches (x1024 frames) decoded per step; 192 = one k_decode_st wave (64 frames) "
-                         "per resident slot (256 CUs x 12 waves), 576 = three such rounds (DESIGN.md section 5)")
+    ap.add_argument("--batches", type=int, default=1024,
+                    help="C2 batches (x1024 frames) decoded per step; 128 = one k_decode_st wave (64 frames) "
+                         "per resident slot (256 CUs x 8 waves); 1024 = eight such rounds (DESIGN.md section 5)")
     ap.add_argument("--frames", type=int, default=1024, help="frames per batch (BASELINE C2: 1024)")
     ap.add_argument("--groups", type=int, default=1,
                     help="pipeline groups: k_parse of group g+1 overlaps k_decode of group g (1 = serial)")
