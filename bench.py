@@ -52,6 +52,7 @@ def parse_args():
                     help="host threads for the multi-thread CPU baseline (0: min(16, cpu count))")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-resident) measurement")
     ap.add_argument("--no-index", action="store_true", help="skip the frame-indexer (bnflac_index_stream) timing")
+    ap.add_argument("--no-reader", action="store_true", help="skip the streaming-reader (bnflac_reader_*) timing")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--stats", action="store_true", help="report k_decode event counters (one extra step)")
     ap.add_argument("--ablate", default=None,
@@ -168,6 +169,24 @@ def index_leg(torch, dev, libflac, dec, data, offs, sp, reps=5):
     return {"ms": round(ms, 4), "GB_per_s": round(n / (ms * 1e-3) / 1e9, 2), "frames": nf, "stream_bytes": n,
             "matches_generator_offsets": match,
             "note": "one C2 stream: sync scan + k_parse of every candidate + CRC-16 chain (one host sync)"}
+
+
+def reader_leg(libflac, data, pcm_ref: bytes, samples: int, reps=3, chunk=16384):
+    """bnflac_reader over one whole C2 stream held in host memory: open
+    (H2D, frame index, decode-ahead) + Read() in OpenAL-sized 16 KiB pieces until the end.
+    Host-link and Python-call bound; reported beside `value`, not part of it."""
+    best, ok = None, True
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = libflac.Reader(data, libflac.OUT_FLACDECODER)
+        got = r.read_all(chunk)
+        r.close()
+        el = time.perf_counter() - t0
+        ok = ok and got == pcm_ref
+        best = el if best is None else min(best, el)
+    return {"value": round(samples / best / 1e6, 2), "unit": "MSamples/s", "ms": round(best * 1e3, 2),
+            "bitexact": bool(ok), "read_bytes": chunk,
+            "note": "host bytes -> bnflac_reader_open (H2D, index, decode-ahead) -> Read() x 16 KiB until EOS"}
 
 
 def main():
@@ -364,6 +383,8 @@ def main():
         line["ablation"] = abl
     if rank == 0 and not args.no_index:
         line["indexer"] = index_leg(torch, dev, libflac, dec, data, offs, sp)
+    if rank == 0 and not args.no_reader:
+        line["reader"] = reader_leg(libflac, data, s.pcm.astype("<i2").tobytes(), samples_per_batch)
     if rank == 0 and not args.no_pcie:
         line["pcie_inclusive"] = pcie_inclusive(args, torch, dev, libflac, dec, data, offs, sp, p, s,
                                                 pcm_bytes_per_batch, samples_per_batch)

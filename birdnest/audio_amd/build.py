@@ -18,7 +18,8 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "lib")
 INCLUDE = os.path.join(ROOT, "include")
 
-HIP_SOURCES = [os.path.join(CSRC, "bnflac_kernels.hip"), os.path.join(CSRC, "bnflac_runtime.cpp")]
+HIP_SOURCES = [os.path.join(CSRC, "bnflac_kernels.hip"), os.path.join(CSRC, "bnflac_runtime.cpp"),
+               os.path.join(CSRC, "bnflac_reader.cpp")]
 HIP_HEADERS = [os.path.join(CSRC, "bnflac_device.h"), os.path.join(CSRC, "bnflac_md5.h"), os.path.join(INCLUDE, "bnflac.h"),
                os.path.join(INCLUDE, "FLAC_compat.h")]
 SYNTH_SOURCES = [os.path.join(CSRC, "synth", "bnflac_synth.c")]
@@ -60,9 +61,10 @@ def build_hip(force=False, verbose=False):
             if only is None or tu in only or not os.path.exists(o):
                 jobs.append(base + [f"-DBNF_TU={tu}", "-c", HIP_SOURCES[0], "-o", o])
             objs.append(o)
-        o = os.path.join(objdir, "bnflac_runtime.o")
-        jobs.append(base + ["-c", HIP_SOURCES[1], "-o", o])
-        objs.append(o)
+        for src in HIP_SOURCES[1:]:
+            o = os.path.join(objdir, os.path.splitext(os.path.basename(src))[0] + ".o")
+            jobs.append(base + ["-c", src, "-o", o])
+            objs.append(o)
         procs = []
         for cmd in jobs:
             if verbose:

@@ -1,0 +1,297 @@
+/*
+ * bnflac_reader.cpp -- streaming PCM reader over a whole FLAC stream.
+ *
+ * The fast path under FLACDecoder.Read (FLACDecoder.cs:124-205) and the OpenAL buffer
+ * fill (OpenALDemo/Program.cs:33-38, StreamingPlayer.cs:424-464): the caller asks for
+ * `count` bytes of packed PCM at a time (4 x 16 KiB for OpenAL) and gets exactly the byte
+ * sequence FLACDecoder.CopyTo would produce.
+ *
+ * On open the compressed stream goes to HBM once, bnflac_index_stream finds its frames,
+ * and the decode then runs ahead of the reader in windows of frames: window w+1 is decoded
+ * and copied into one slot of a pinned host ring while the caller drains window w from the
+ * other.  Reads are memcpy from pinned memory; the GPU work and the D2H copies overlap
+ * them.  A stream that is not intact (the frame chain ends before STREAMINFO's total, a
+ * frame fails its CRC, or a frame needs the libFLAC error path) is refused at the point
+ * it is reached, with bnflac_reader_last_error() saying why: the libFLAC stream API is the path
+ * for damaged streams.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/bnflac.h"
+
+namespace {
+
+thread_local std::string g_rerr;
+int rfail(const std::string &m) {
+    g_rerr = m;
+    return -1;
+}
+
+/* STREAMINFO and the first frame offset from the metadata blocks (read_metadata_) */
+bool parse_metadata(const uint8_t *d, uint64_t n, bnflac_stream_params &sp, uint64_t &first) {
+    if (n < 8 || memcmp(d, "fLaC", 4) != 0) return false;
+    uint64_t p = 4;
+    bool have = false;
+    for (;;) {
+        if (p + 4 > n) return false;
+        const uint32_t hdr = d[p], len = ((uint32_t)d[p + 1] << 16) | ((uint32_t)d[p + 2] << 8) | d[p + 3];
+        if ((hdr & 0x7F) == 0 && len >= 34 && p + 4 + 34 <= n) {
+            const uint8_t *s = d + p + 4;
+            sp.has_stream_info = 1;
+            sp.min_blocksize = ((uint32_t)s[0] << 8) | s[1];
+            sp.max_blocksize = ((uint32_t)s[2] << 8) | s[3];
+            uint64_t x = 0;
+            for (int i = 10; i < 18; i++) x = (x << 8) | s[i];
+            sp.sample_rate = (uint32_t)(x >> 44);
+            sp.channels = (uint32_t)((x >> 41) & 7) + 1;
+            sp.bps = (uint32_t)((x >> 36) & 31) + 1;
+            sp.total_samples = x & ((1ull << 36) - 1);
+            have = true;
+        }
+        p += 4 + (uint64_t)len;
+        if (hdr & 0x80) break;
+    }
+    first = p;
+    return have && p <= n;
+}
+
+} // namespace
+
+struct bnflac_reader {
+    bnflac_ctx *ctx = nullptr;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bnflac_stream_params sp{};
+    int fmt = BNFLAC_OUT_FLACDECODER;
+    uint32_t stride = 0;
+    uint64_t nbytes = 0;
+    void *d_bytes = nullptr, *d_offs = nullptr, *d_os = nullptr, *d_info = nullptr, *d_out = nullptr, *d_n = nullptr;
+    uint32_t nframes = 0;
+    std::vector<uint64_t> os; /* out_sample per frame, + end */
+    uint32_t window = 256;    /* frames per window */
+    uint32_t nwin = 0;
+    /* pinned ring: two slots, each one window of PCM */
+    uint8_t *ring[2] = {nullptr, nullptr};
+    size_t slot_bytes = 0;
+    hipEvent_t done[2] = {nullptr, nullptr};
+    uint32_t slot_win[2] = {~0u, ~0u}; /* window held (or in flight) in each slot */
+    uint32_t cur = 0;                  /* window being read */
+    uint64_t cur_pos = 0;              /* bytes of it already returned */
+    uint64_t total_bytes = 0, returned = 0;
+    std::vector<bnflac_frame_info> winfo;
+    bool failed = false;
+};
+
+namespace {
+
+uint64_t win_bytes(const bnflac_reader *r, uint32_t w) {
+    const uint32_t f0 = w * r->window, f1 = std::min(r->nframes, f0 + r->window);
+    return (r->os[f1] - r->os[f0]) * r->stride;
+}
+
+/* decode window w and copy it into its slot; asynchronous on r->stream */
+int issue_window(bnflac_reader *r, uint32_t w) {
+    if (w >= r->nwin) return 0;
+    const uint32_t slot = w & 1u;
+    const uint32_t f0 = w * r->window, nf = std::min(r->nframes, f0 + r->window) - f0;
+    bnflac_frame_info *info = (bnflac_frame_info *)r->d_info + f0;
+    if (bnflac_decode_parsed(r->ctx, (const uint8_t *)r->d_bytes, r->nbytes, nf, &r->sp, r->fmt, (uint8_t *)r->d_out,
+                             r->total_bytes, info, r->stream))
+        return rfail(std::string("bnflac_reader: ") + bnflac_last_error());
+    const uint64_t b0 = r->os[f0] * r->stride, nb = win_bytes(r, w);
+    if (nb && hipMemcpyAsync(r->ring[slot], (const uint8_t *)r->d_out + b0, nb, hipMemcpyDeviceToHost, r->stream) != hipSuccess)
+        return rfail("bnflac_reader: D2H copy failed");
+    if (hipMemcpyAsync(r->winfo.data() + (size_t)slot * r->window, info, sizeof(bnflac_frame_info) * nf,
+                       hipMemcpyDeviceToHost, r->stream) != hipSuccess)
+        return rfail("bnflac_reader: D2H copy failed");
+    if (hipEventRecord(r->done[slot], r->stream) != hipSuccess) return rfail("bnflac_reader: event record failed");
+    r->slot_win[slot] = w;
+    return 0;
+}
+
+/* wait for window w and check every frame of it decoded cleanly */
+int land_window(bnflac_reader *r, uint32_t w) {
+    const uint32_t slot = w & 1u;
+    if (r->slot_win[slot] != w) return rfail("bnflac_reader: window not issued");
+    if (hipEventSynchronize(r->done[slot]) != hipSuccess) return rfail("bnflac_reader: HIP error while decoding");
+    const uint32_t f0 = w * r->window, nf = std::min(r->nframes, f0 + r->window) - f0;
+    for (uint32_t i = 0; i < nf; i++) {
+        const bnflac_frame_info &fi = r->winfo[(size_t)slot * r->window + i];
+        if (fi.status == 3 && (fi.flags & 4u))
+            return rfail("bnflac_reader: frame at byte " + std::to_string(fi.frame_off) +
+                         " cannot be carried by this output layout");
+        if (fi.status != 0 || !fi.crc_ok)
+            return rfail("bnflac_reader: frame at byte " + std::to_string(fi.frame_off) +
+                         " is damaged (use the libFLAC stream API for damaged streams)");
+    }
+    return 0;
+}
+
+void release(bnflac_reader *r) {
+    if (r->stream) (void)hipStreamSynchronize(r->stream);
+    for (void *p : {r->d_bytes, r->d_offs, r->d_os, r->d_info, r->d_out, r->d_n})
+        if (p) (void)hipFree(p);
+    for (int i = 0; i < 2; i++) {
+        if (r->ring[i]) (void)hipHostFree(r->ring[i]);
+        if (r->done[i]) (void)hipEventDestroy(r->done[i]);
+    }
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    if (r->ctx) bnflac_ctx_destroy(r->ctx);
+    delete r;
+}
+
+} // namespace
+
+extern "C" {
+
+BNFLAC_API const char *bnflac_reader_last_error(void) { return g_rerr.c_str(); }
+
+BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nbytes, int out_format,
+                                  uint32_t window_frames, bnflac_reader **out) {
+    if (!out) return rfail("bnflac_reader_open: null out");
+    *out = nullptr;
+    if (!bytes) return rfail("bnflac_reader_open: null bytes");
+    if (out_format < 0 || out_format > 3) return rfail("bnflac_reader_open: bad out_format");
+    bnflac_reader *r = new bnflac_reader();
+    r->device = device;
+    r->fmt = out_format;
+    if (window_frames) r->window = window_frames;
+    uint64_t first = 0;
+    if (!parse_metadata(bytes, nbytes, r->sp, first)) {
+        release(r);
+        return rfail("bnflac_reader_open: no fLaC marker / STREAMINFO (use the libFLAC stream API)");
+    }
+    if (r->sp.channels < 1 || r->sp.channels > 8) {
+        release(r);
+        return rfail("bnflac_reader_open: bad channel count");
+    }
+    if (out_format == BNFLAC_OUT_FLACDECODER && r->sp.bps != 16) { /* FLACDecoder.cs:526-529 aborts on these */
+        release(r);
+        return rfail("bnflac_reader_open: FLACDecoder layout needs 16-bit samples, stream has " +
+                     std::to_string(r->sp.bps));
+    }
+    if (bnflac_ctx_create(device, &r->ctx)) {
+        const std::string e = bnflac_last_error();
+        r->ctx = nullptr;
+        release(r);
+        return rfail("bnflac_reader_open: " + e);
+    }
+    r->stride = bnflac_out_stride(out_format, &r->sp);
+    r->nbytes = nbytes;
+    const size_t padded = (size_t)((nbytes + 15) & ~15ull) + 16;
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(nbytes / 8 + 16, 1u << 30); /* a frame is >= 9 bytes */
+    if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&r->d_bytes, padded) != hipSuccess || hipMalloc(&r->d_offs, 8ull * cap) != hipSuccess ||
+        hipMalloc(&r->d_os, 8ull * cap) != hipSuccess || hipMalloc(&r->d_info, sizeof(bnflac_frame_info) * cap) != hipSuccess ||
+        hipMalloc(&r->d_n, 16) != hipSuccess) {
+        release(r);
+        return rfail("bnflac_reader_open: out of device memory");
+    }
+    /* one H2D of the whole stream; the tail padding is zero */
+    if (hipMemsetAsync((uint8_t *)r->d_bytes + (nbytes & ~15ull), 0, padded - (nbytes & ~15ull), r->stream) != hipSuccess ||
+        hipMemcpyAsync(r->d_bytes, bytes, nbytes, hipMemcpyHostToDevice, r->stream) != hipSuccess) {
+        release(r);
+        return rfail("bnflac_reader_open: H2D copy failed");
+    }
+    if (bnflac_index_stream(r->ctx, (const uint8_t *)r->d_bytes, nbytes, first, &r->sp, (uint64_t *)r->d_offs,
+                            (uint64_t *)r->d_os, (bnflac_frame_info *)r->d_info, cap, (uint32_t *)r->d_n, r->stream)) {
+        const std::string e = bnflac_last_error();
+        release(r);
+        return rfail("bnflac_reader_open: " + e);
+    }
+    uint32_t nf = 0;
+    if (hipMemcpyAsync(&nf, r->d_n, 4, hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
+        hipStreamSynchronize(r->stream) != hipSuccess || nf > cap) {
+        release(r);
+        return rfail("bnflac_reader_open: frame index failed");
+    }
+    r->nframes = nf;
+    r->os.resize((size_t)nf + 1);
+    if (nf && hipMemcpy(r->os.data(), r->d_os, 8ull * nf, hipMemcpyDeviceToHost) != hipSuccess) {
+        release(r);
+        return rfail("bnflac_reader_open: D2H copy failed");
+    }
+    /* the end of the last frame: its blocksize from its record */
+    uint64_t end = 0;
+    if (nf) {
+        bnflac_frame_info last;
+        if (hipMemcpy(&last, (bnflac_frame_info *)r->d_info + (nf - 1), sizeof last, hipMemcpyDeviceToHost) != hipSuccess) {
+            release(r);
+            return rfail("bnflac_reader_open: D2H copy failed");
+        }
+        end = r->os[nf - 1] + last.blocksize;
+    }
+    r->os[nf] = end;
+    if (r->sp.total_samples && end != r->sp.total_samples) {
+        release(r);
+        return rfail("bnflac_reader_open: the frame chain covers " + std::to_string(end) + " of " +
+                     std::to_string(r->sp.total_samples) + " samples (damaged stream: use the libFLAC stream API)");
+    }
+    r->total_bytes = end * r->stride;
+    r->nwin = (nf + r->window - 1) / r->window;
+    for (uint32_t w = 0; w < r->nwin; w++) r->slot_bytes = std::max<size_t>(r->slot_bytes, win_bytes(r, w));
+    r->winfo.resize((size_t)2 * r->window);
+    if (hipMalloc(&r->d_out, std::max<uint64_t>(r->total_bytes, 16)) != hipSuccess ||
+        hipHostMalloc((void **)&r->ring[0], std::max<size_t>(r->slot_bytes, 16), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&r->ring[1], std::max<size_t>(r->slot_bytes, 16), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&r->done[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->done[1], hipEventDisableTiming) != hipSuccess) {
+        release(r);
+        return rfail("bnflac_reader_open: out of memory");
+    }
+    /* decode-ahead: the first two windows */
+    if (issue_window(r, 0) || issue_window(r, 1)) {
+        release(r);
+        return -1;
+    }
+    *out = r;
+    return 0;
+}
+
+BNFLAC_API int bnflac_reader_params(const bnflac_reader *r, bnflac_stream_params *sp, uint64_t *total_bytes,
+                                    uint32_t *nframes) {
+    if (!r) return rfail("bnflac_reader_params: null reader");
+    if (sp) *sp = r->sp;
+    if (total_bytes) *total_bytes = r->total_bytes;
+    if (nframes) *nframes = r->nframes;
+    return 0;
+}
+
+BNFLAC_API int64_t bnflac_reader_read(bnflac_reader *r, uint8_t *buf, uint64_t count) {
+    if (!r) return rfail("bnflac_reader_read: null reader");
+    if (r->failed) return rfail("bnflac_reader_read: reader failed earlier");
+    if (!buf && count) return rfail("bnflac_reader_read: null buffer");
+    uint64_t done = 0;
+    while (done < count && r->cur < r->nwin) {
+        const uint32_t w = r->cur, slot = w & 1u;
+        if (r->cur_pos == 0 && land_window(r, w)) {
+            r->failed = true;
+            return -1;
+        }
+        const uint64_t wb = win_bytes(r, w), take = std::min<uint64_t>(count - done, wb - r->cur_pos);
+        memcpy(buf + done, r->ring[slot] + r->cur_pos, take);
+        done += take;
+        r->cur_pos += take;
+        if (r->cur_pos == wb) { /* window drained: its slot takes the window after the next */
+            r->cur++;
+            r->cur_pos = 0;
+            if (issue_window(r, w + 2)) {
+                r->failed = true;
+                return -1;
+            }
+        }
+    }
+    r->returned += done;
+    return (int64_t)done;
+}
+
+BNFLAC_API void bnflac_reader_close(bnflac_reader *r) {
+    if (r) release(r);
+}
+
+} /* extern "C" */

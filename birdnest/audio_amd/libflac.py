@@ -126,6 +126,8 @@ BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error",
                  "bnflac_index_frames", "bnflac_decode_frames", "bnflac_parse_frames", "bnflac_decode_parsed",
                  "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats",
                  "bnflac_md5_interleaved32", "bnflac_index_stream"]
+READER_SYMBOLS = ["bnflac_reader_open", "bnflac_reader_params", "bnflac_reader_read", "bnflac_reader_close",
+                  "bnflac_reader_last_error"]
 
 _LIB = None
 
@@ -181,6 +183,14 @@ def load() -> ctypes.CDLL:
     L.FLAC__stream_decoder_get_md5_checking.argtypes = [p]
     L.bnflac_index_stream.restype = i
     L.bnflac_index_stream.argtypes = [p, p, ctypes.c_uint64, ctypes.c_uint64, p, p, p, p, ctypes.c_uint32, p, p]
+    L.bnflac_reader_open.restype = i
+    L.bnflac_reader_open.argtypes = [i, p, ctypes.c_uint64, i, ctypes.c_uint32, ctypes.POINTER(p)]
+    L.bnflac_reader_params.restype = i
+    L.bnflac_reader_params.argtypes = [p, p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]
+    L.bnflac_reader_read.restype = ctypes.c_int64
+    L.bnflac_reader_read.argtypes = [p, p, ctypes.c_uint64]
+    L.bnflac_reader_close.argtypes = [p]
+    L.bnflac_reader_last_error.restype = ctypes.c_char_p
     L.bnflac_md5_interleaved32.restype = i
     L.bnflac_md5_interleaved32.argtypes = [p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, p]
     _LIB = L
@@ -391,6 +401,54 @@ class BatchDecoder:
                                          self._stream(stream))
         if rc != 0:
             raise RuntimeError(self.L.bnflac_last_error().decode())
+
+
+class Reader:
+    """Streaming PCM reader (include/bnflac.h part 3): Read(buffer, offset, count) like
+    FLACDecoder.Read (FLACDecoder.cs:124-205), backed by GPU decode-ahead."""
+
+    def __init__(self, data: bytes, out_format: int = OUT_FLACDECODER, window_frames: int = 0, device: int = 0):
+        self.L = load()
+        self._data = np.frombuffer(bytes(data), dtype=np.uint8)
+        h = ctypes.c_void_p()
+        rc = self.L.bnflac_reader_open(device, self._data.ctypes.data, self._data.size, out_format, window_frames,
+                                       ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(self.L.bnflac_reader_last_error().decode())
+        self.h = h
+        sp = StreamParams()
+        tb, nf = ctypes.c_uint64(), ctypes.c_uint32()
+        self.L.bnflac_reader_params(self.h, ctypes.byref(sp), ctypes.byref(tb), ctypes.byref(nf))
+        self.stream_params, self.total_bytes, self.nframes = sp, int(tb.value), int(nf.value)
+
+    def Read(self, buffer: bytearray, offset: int, count: int) -> int:
+        if offset < 0 or count < 0 or offset + count > len(buffer):
+            raise ValueError("offset/count outside the buffer")
+        view = (ctypes.c_uint8 * len(buffer)).from_buffer(buffer)
+        n = self.L.bnflac_reader_read(self.h, ctypes.addressof(view) + offset, count)
+        if n < 0:
+            raise RuntimeError(self.L.bnflac_reader_last_error().decode())
+        return int(n)
+
+    def read_all(self, chunk: int = 16384) -> bytes:
+        out = bytearray()
+        buf = bytearray(chunk)
+        while True:
+            n = self.Read(buf, 0, chunk)
+            if n == 0:
+                return bytes(out)
+            out += buf[:n]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.bnflac_reader_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def info_array(raw: np.ndarray) -> np.ndarray:

@@ -189,6 +189,28 @@ BNFLAC_API uint32_t bnflac_out_stride(int out_format, const bnflac_stream_params
 BNFLAC_API int bnflac_md5_interleaved32(const int32_t *pcm, uint64_t nsamples, uint32_t channels, uint32_t bps,
                                         uint8_t out_md5[16]);
 
+/* ======================== Part 3: streaming reader ======================= */
+
+/* The fast path under FLACDecoder.Read (FLACDecoder.cs:124-205) and OpenAL's buffer fill
+ * (OpenALDemo/Program.cs:33-38): a whole FLAC stream in host memory in, packed PCM out in
+ * caller-sized pieces.  open() copies the stream to HBM once, indexes its frames on the GPU
+ * (bnflac_index_stream) and starts decoding ahead in windows of `window_frames` frames
+ * (0: 256) into a two-slot pinned host ring; read() copies from the ring while the next
+ * window decodes.  The bytes are those of out_format (BNFLAC_OUT_FLACDECODER: what
+ * FLACDecoder.CopyTo yields).  Intact streams only: open() or read() returns -1 at the
+ * first sign of damage (frame chain short of STREAMINFO's total, CRC failure), with the
+ * reason in bnflac_reader_last_error(); the libFLAC stream API (part 1) handles those. */
+typedef struct bnflac_reader bnflac_reader;
+BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nbytes, int out_format,
+                                  uint32_t window_frames, bnflac_reader **out);
+/* STREAMINFO, total PCM bytes the reader will return, frames found.  Any pointer may be NULL. */
+BNFLAC_API int bnflac_reader_params(const bnflac_reader *reader, bnflac_stream_params *sp, uint64_t *total_bytes,
+                                    uint32_t *nframes);
+/* Up to count bytes into buf; returns the number copied (0: end of stream) or -1. */
+BNFLAC_API int64_t bnflac_reader_read(bnflac_reader *reader, uint8_t *buf, uint64_t count);
+BNFLAC_API void bnflac_reader_close(bnflac_reader *reader);
+BNFLAC_API const char *bnflac_reader_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -504,3 +504,75 @@ def test_stereo_handback_matches(gpu, cfg):
     assert out_a.tobytes() == out_b.tobytes()
     keep = [n for n in info_a.dtype.names if n != "flags"]
     assert all(np.array_equal(info_a[n], info_b[n]) for n in keep)
+
+
+@pytest.mark.parametrize("stereo_mode", [1, 2, 3])
+def test_stereo_side_beyond_int16_handed_back(gpu, stereo_mode):
+    """k_decode_st's dot2 predictor is exact only while samples fit int16.  Loud,
+    weakly correlated channels push the 17-bit side channel past that: those frames must be
+    handed back (BNF_FL_REDO) and come out of k_decode<8> bit-exact."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    p = synth.config("C2", nframes=40, stereo_mode=stereo_mode, level=0.9, noise=0.5)
+    s = synth.encode(p)
+    side = s.pcm[:, 0].astype(np.int64) - s.pcm[:, 1]
+    assert np.abs(side).max() > 32767  # the fixture does leave int16
+    out, info, sp = _decode_batch(gpu, s.data.tobytes(), s.frame_offsets, libflac.OUT_INTERLEAVED32)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    assert (info["flags"] & FL_REDO).any(), info["flags"]
+    assert np.array_equal(out.view("<i4").reshape(-1, 2), s.pcm)
+
+
+# ------------------------------------------------- streaming reader (SURVEY.md 8f-2)
+@pytest.mark.parametrize("name", [k for k, v in GOLD.items() if v["kind"] in ("roundtrip", "rfc")])
+def test_reader_matches_flacdecoder_copyto(gpu, name):
+    """bnflac_reader yields the bytes FLACDecoder.CopyTo yields (the libFLAC-API mirror),
+    read in OpenAL-sized 16 KiB pieces."""
+    from birdnest.audio_amd import flac_decoder
+    torch, libflac, _ = gpu
+    data = _read(name)
+    rc, pk, msg, fmt = flac_decoder.copy_to_bytes(data)
+    if rc != 0 or fmt[2] != 16:
+        pytest.skip(f"FLACDecoder does not yield this stream: {msg or fmt}")
+    r = libflac.Reader(data, libflac.OUT_FLACDECODER, window_frames=5)
+    try:
+        assert r.total_bytes == len(pk)
+        assert r.read_all(16384) == pk
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("window,chunk", [(256, 16384), (7, 1000), (1, 4096 * 4 + 3)])
+def test_reader_c2_windows_and_chunks(gpu, window, chunk):
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    s = synth.encode(synth.config("C2", nframes=96))
+    r = libflac.Reader(s.data.tobytes(), libflac.OUT_FLACDECODER, window_frames=window)
+    try:
+        assert r.nframes == 96
+        got = r.read_all(chunk)
+        assert got == s.pcm.astype("<i2").tobytes()
+        buf = bytearray(10)
+        assert r.Read(buf, 0, 10) == 0  # end of stream
+    finally:
+        r.close()
+    r = libflac.Reader(s.data.tobytes(), libflac.OUT_INTERLEAVED32, window_frames=window)
+    try:
+        assert np.array_equal(np.frombuffer(r.read_all(chunk), dtype="<i4").reshape(-1, 2), s.pcm)
+    finally:
+        r.close()
+
+
+def test_reader_refuses_damaged_stream(gpu):
+    torch, libflac, _ = gpu
+    data = _read("err_crc16_mismatch")
+    with pytest.raises(RuntimeError, match="damaged|covers"):
+        r = libflac.Reader(data, libflac.OUT_FLACDECODER, window_frames=2)
+        try:
+            r.read_all(16384)
+        finally:
+            r.close()
+    with pytest.raises(RuntimeError, match="fLaC"):
+        libflac.Reader(b"not a flac stream at all", libflac.OUT_FLACDECODER)
+    with pytest.raises(RuntimeError, match="16-bit"):
+        libflac.Reader(_read("c3_lpc12_ms_wasted"), libflac.OUT_FLACDECODER)

@@ -24,7 +24,7 @@ fi
 if [[ $STEPS == *prof* ]]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- \
-      python3 "$ROOT/bench.py" ${PROF_ARGS:---steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-index} > "$OUT/prof_$TAG.log" 2>&1
+      python3 "$ROOT/bench.py" ${PROF_ARGS:---steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-index --no-reader} > "$OUT/prof_$TAG.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof_$TAG.log"
   [ $rc -eq 0 ] || stop rocprof $rc
 fi

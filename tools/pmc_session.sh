@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/pmc_${TAG:-r1}
 mkdir -p "$OUT"
-ARGS=${PMC_BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-pcie --no-index}
+ARGS=${PMC_BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-pcie --no-index --no-reader}
 cd /tmp && export TMPDIR=/tmp
 i=0
 while IFS= read -r ctrs; do
