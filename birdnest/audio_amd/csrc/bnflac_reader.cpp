@@ -290,6 +290,34 @@ BNFLAC_API int64_t bnflac_reader_read(bnflac_reader *r, uint8_t *buf, uint64_t c
     return (int64_t)done;
 }
 
+/* FLACFileReader.Position / seek_absolute (FLACFileReader.cs:109-137,295-299): the next read
+ * starts at sample `sample` (per channel).  The frame holding it is found in the index
+ * (binary search over the running sample counts); its window and the next are decoded
+ * again and the reader resumes inside the first. */
+BNFLAC_API int bnflac_reader_seek(bnflac_reader *r, uint64_t sample) {
+    if (!r) return rfail("bnflac_reader_seek: null reader");
+    if (r->failed) return rfail("bnflac_reader_seek: reader failed earlier");
+    const uint64_t total = r->os[r->nframes];
+    if (sample >= total) return rfail("bnflac_reader_seek: sample past the end of the stream");
+    if (hipStreamSynchronize(r->stream) != hipSuccess) return rfail("bnflac_reader_seek: HIP error");
+    const uint32_t f = (uint32_t)(std::upper_bound(r->os.begin(), r->os.begin() + r->nframes, sample) - r->os.begin()) - 1u;
+    const uint32_t w = f / r->window;
+    r->slot_win[0] = r->slot_win[1] = ~0u;
+    if (issue_window(r, w) || issue_window(r, w + 1)) {
+        r->failed = true;
+        return -1;
+    }
+    r->cur = w;
+    r->cur_pos = 0;
+    if (land_window(r, w)) {
+        r->failed = true;
+        return -1;
+    }
+    r->cur_pos = (sample - r->os[(size_t)w * r->window]) * r->stride;
+    r->returned = sample * r->stride;
+    return 0;
+}
+
 BNFLAC_API void bnflac_reader_close(bnflac_reader *r) {
     if (r) release(r);
 }

@@ -127,7 +127,7 @@ BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error",
                  "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats",
                  "bnflac_md5_interleaved32", "bnflac_index_stream"]
 READER_SYMBOLS = ["bnflac_reader_open", "bnflac_reader_params", "bnflac_reader_read", "bnflac_reader_close",
-                  "bnflac_reader_last_error"]
+                  "bnflac_reader_last_error", "bnflac_reader_seek"]
 
 _LIB = None
 
@@ -190,6 +190,8 @@ def load() -> ctypes.CDLL:
     L.bnflac_reader_read.restype = ctypes.c_int64
     L.bnflac_reader_read.argtypes = [p, p, ctypes.c_uint64]
     L.bnflac_reader_close.argtypes = [p]
+    L.bnflac_reader_seek.restype = i
+    L.bnflac_reader_seek.argtypes = [p, ctypes.c_uint64]
     L.bnflac_reader_last_error.restype = ctypes.c_char_p
     L.bnflac_md5_interleaved32.restype = i
     L.bnflac_md5_interleaved32.argtypes = [p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, p]
@@ -429,6 +431,11 @@ class Reader:
         if n < 0:
             raise RuntimeError(self.L.bnflac_reader_last_error().decode())
         return int(n)
+
+    def Seek(self, sample: int):
+        """Next Read starts at this sample (per channel): FLACFileReader.Position."""
+        if self.L.bnflac_reader_seek(self.h, sample) != 0:
+            raise RuntimeError(self.L.bnflac_reader_last_error().decode())
 
     def read_all(self, chunk: int = 16384) -> bytes:
         out = bytearray()

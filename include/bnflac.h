@@ -208,6 +208,10 @@ BNFLAC_API int bnflac_reader_params(const bnflac_reader *reader, bnflac_stream_p
                                     uint32_t *nframes);
 /* Up to count bytes into buf; returns the number copied (0: end of stream) or -1. */
 BNFLAC_API int64_t bnflac_reader_read(bnflac_reader *reader, uint8_t *buf, uint64_t count);
+/* Position the reader so the next read starts at `sample` (per channel), like
+ * FLACFileReader.Position / seek_absolute (FLACFileReader.cs:109-137,295-299).  0 or -1
+ * (sample past the end, or damage in the target window). */
+BNFLAC_API int bnflac_reader_seek(bnflac_reader *reader, uint64_t sample);
 BNFLAC_API void bnflac_reader_close(bnflac_reader *reader);
 BNFLAC_API const char *bnflac_reader_last_error(void);
 

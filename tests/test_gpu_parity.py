@@ -576,3 +576,27 @@ def test_reader_refuses_damaged_stream(gpu):
         libflac.Reader(b"not a flac stream at all", libflac.OUT_FLACDECODER)
     with pytest.raises(RuntimeError, match="16-bit"):
         libflac.Reader(_read("c3_lpc12_ms_wasted"), libflac.OUT_FLACDECODER)
+
+
+def test_reader_seek(gpu):
+    """bnflac_reader_seek: the next read starts at the target sample (FLACFileReader.Position),
+    across frame and window boundaries, mid-frame, and at the last sample."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    s = synth.encode(synth.config("C4", nframes=120))
+    ref = s.pcm.astype("<i2").tobytes()
+    n = s.pcm.shape[0]
+    r = libflac.Reader(s.data.tobytes(), libflac.OUT_FLACDECODER, window_frames=9)
+    try:
+        buf = bytearray(5000)
+        for target in (0, 1, 4095, n // 3, n // 2 + 7, n - 1, 12345):
+            r.Seek(target)
+            got = r.Read(buf, 0, len(buf))
+            want = ref[target * 4: target * 4 + len(buf)]
+            assert got == len(want) and bytes(buf[:got]) == want, target
+        r.Seek(n - 100)
+        assert r.read_all(64) == ref[(n - 100) * 4:]
+        with pytest.raises(RuntimeError, match="past the end"):
+            r.Seek(n)
+    finally:
+        r.close()
