@@ -12,8 +12,11 @@ value      = decoded samples (blocksize x channels) per s
              whole job over all ranks (weak scaling: every rank decodes its own batches).
 roofline   = the dominant kernel (k_decode): algorithmic bytes (compressed frame bytes +
              PCM bytes written) / its HIP-event-timed average duration, vs 8 TB/s HBM.
-cpu_baseline = the CPU restatement (oracle/: libFLAC 1.2.1 decode + FLACDecoder pack),
-             one thread, on a bounded sample of the same frames.
+cpu_baseline = the CPU restatement (oracle/: libFLAC 1.2.1 decode + FLACDecoder pack) on
+             min(16, cpu count) threads, plus a 1-thread figure, on a bounded sample of
+             the same frames.
+Beside the metric (rank 0): indexer (bnflac_index_stream over one stream), reader
+(bnflac_reader_* from host bytes to 16 KiB reads), pcie_inclusive (host-resident batches).
 
     python bench.py [--gpus N --steps K --warmup W --batches B]
     torchrun --nproc-per-node N bench.py --gpus N ...
