@@ -600,3 +600,31 @@ def test_reader_seek(gpu):
             r.Seek(n)
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_stereo_fast_path_random_sweep(gpu, seed):
+    """Randomised 16-bit stereo streams through k_decode_st (and its hand-backs): blocksize,
+    predictor type/order, partition order, RICE2, escapes, wasted bits, stereo mode, level
+    and noise all drawn per seed; output must equal the generator's source PCM."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    rng = np.random.default_rng(1000 + seed)
+    bs = int(rng.choice([1152, 2048, 4096, 4608, 576 * 7]))
+    kw = dict(nframes=int(rng.integers(40, 140)), blocksize=bs, last_blocksize=int(rng.integers(64, bs)),
+              subframe_mode=int(rng.choice([synth.SUB_LPC, synth.SUB_FIXED, synth.SUB_LPC])),
+              order=int(rng.integers(1, 9)), partition_order=int(rng.choice([-1, 0, 2, 4, 6])),
+              stereo_mode=int(rng.integers(0, 5)), rice2=int(rng.integers(0, 2)),
+              escape_permille=int(rng.choice([0, 0, 20])), wasted_bits_max=int(rng.choice([0, 0, 3])),
+              level=float(rng.uniform(0.05, 0.9)), noise=float(rng.choice([0.0005, 0.006, 0.05])),
+              seed=50 + seed, prec_clamp=int(rng.integers(0, 2)))
+    if kw["subframe_mode"] == synth.SUB_FIXED:
+        kw["order"] = int(rng.integers(0, 5))
+    s = synth.encode(synth.config("C2", **kw))
+    for fmt in (libflac.OUT_FLACDECODER, libflac.OUT_INTERLEAVED32):
+        out, info, sp = _decode_batch(gpu, s.data.tobytes(), s.frame_offsets, fmt)
+        assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all(), kw
+        if fmt == libflac.OUT_INTERLEAVED32:
+            assert np.array_equal(out.view("<i4").reshape(-1, 2), s.pcm), kw
+        else:
+            assert out.tobytes() == (s.pcm.astype(np.int64) & 0xFFFF).astype("<u2").tobytes(), kw
