@@ -1314,7 +1314,8 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
             rs.k = h.bps;
             rs.order = h.order;
             rs.porder = h.porder;
-            rs.nparts = 1u << h.porder;
+            /* a CONSTANT subframe has no residual: no partition headers to finish */
+            rs.nparts = (h.type == T_FIXED || h.type == T_LPC) ? 1u << h.porder : 0u;
             rs.psamples = h.porder ? bs >> h.porder : bs - h.order;
             rs.plen = h.rice2 ? 5u : 4u;
             rs.pesc = h.rice2 ? 31u : 15u;

@@ -628,3 +628,21 @@ def test_stereo_fast_path_random_sweep(gpu, seed):
             assert np.array_equal(out.view("<i4").reshape(-1, 2), s.pcm), kw
         else:
             assert out.tobytes() == (s.pcm.astype(np.int64) & 0xFFFF).astype("<u2").tobytes(), kw
+
+
+@pytest.mark.parametrize("kw", [
+    dict(channels=1, bps=16, blocksize=2048, nframes=79, last_blocksize=1591, subframe_mode=4, order=3,
+         partition_order=-1, stereo_mode=0, level=0.0534, noise=0.3, seed=849887222, sample_rate=192000),
+    dict(channels=6, bps=16, blocksize=4096, nframes=42, last_blocksize=1673, subframe_mode=4, order=1,
+         partition_order=1, stereo_mode=0, level=0.374, noise=0.03, seed=455035102, sample_rate=8000),
+])
+def test_constant_last_subframe(gpu, kw):
+    """Regression (found by tools/stress.py): a CONSTANT subframe in the last channel has no
+    residual, so k_decode must not read a partition header after it (that misread the
+    zero padding as LOST_SYNC on tiny constant frames)."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    s = synth.encode(synth.config("C2", **kw))
+    out, info, sp = _decode_batch(gpu, s.data.tobytes(), s.frame_offsets, libflac.OUT_INTERLEAVED32)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all(), info[["status", "err", "flags"]]
+    assert np.array_equal(out.view("<i4").reshape(-1, kw["channels"]), s.pcm)
