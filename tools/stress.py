@@ -95,6 +95,17 @@ def main():
             if not ok:
                 print(i, "fmt", fmt, "PCM differs", flush=True)
                 break
+        if ok and "--index" in sys.argv:  # GPU frame chain == the generator's frame offsets
+            offs_i, _, _, nfi = dec.index_stream(d_bytes, nb, int(s.frame_offsets[0]), sp, nf + 16)
+            if nfi != nf or not np.array_equal(offs_i[:nf].cpu().numpy(), s.frame_offsets.astype(np.int64)):
+                print(i, "index differs", nfi, nf, flush=True)
+                ok = False
+        if ok and "--api" in sys.argv:  # libFLAC-compatible stream API events == the oracle's
+            from birdnest.audio_amd import harness
+            hev, hpcm = harness.run(data, driver=0)
+            if hev != harness.oracle_events_as_tuples(ev) or not np.array_equal(hpcm, opcm):
+                print(i, "stream API differs from the oracle", flush=True)
+                ok = False
         if not ok:
             bad += 1
             print(i, "MISMATCH", kw, flush=True)
