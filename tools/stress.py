@@ -54,6 +54,30 @@ def main():
             print(i, "generator refused", kw, e)
             continue
         data = s.data.tobytes()
+        if "--corrupt" in sys.argv:  # damaged stream: only the stream API's error handling is compared
+            buf = bytearray(data)
+            first = int(s.frame_offsets[0])
+            for _ in range(int(rng.integers(1, 6))):
+                pos = int(rng.integers(first, len(buf)))
+                buf[pos] ^= int(rng.integers(1, 256))
+            if rng.integers(0, 4) == 0:
+                buf = buf[: int(rng.integers(first, len(buf)))]  # truncated too
+            data = bytes(buf)
+            from birdnest.audio_amd import harness
+            ok = True
+            for drv in (0, 1):
+                ev, opcm = oracle.run(data, driver=drv)
+                hev, hpcm = harness.run(data, driver=drv)
+                if hev != harness.oracle_events_as_tuples(ev) or not np.array_equal(hpcm, opcm):
+                    ok = False
+                    print(i, "corrupt stream: stream API differs from the oracle, driver", drv, flush=True)
+                    break
+            if not ok:
+                bad += 1
+                print(i, "MISMATCH", kw, flush=True)
+            if i % 20 == 0:
+                print(i, "ok so far, bad", bad, f"{time.time() - t0:.0f}s", flush=True)
+            continue
         ev, opcm = oracle.run(data)
         ref = oracle.interleave(ev, opcm)
         if ref.shape != s.pcm.shape or not np.array_equal(ref, s.pcm):
