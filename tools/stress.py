@@ -124,6 +124,17 @@ def main():
             if nfi != nf or not np.array_equal(offs_i[:nf].cpu().numpy(), s.frame_offsets.astype(np.int64)):
                 print(i, "index differs", nfi, nf, flush=True)
                 ok = False
+        if ok and "--layouts" in sys.argv and kw["bps"] == 16:  # FLACDecoder bytes == the C# replay
+            orc, oref, omsg, _ = oracle.flacdecoder_copyto(data)
+            if orc == 0:
+                stride = libflac.out_stride(libflac.OUT_FLACDECODER, sp)
+                d_out = torch.zeros(int(s.nsamples) * stride + 64, dtype=torch.uint8, device=dev)
+                d_info = torch.zeros(nf * 128, dtype=torch.uint8, device=dev)
+                dec.decode_frames(d_bytes, nb, offs, nf, sp, libflac.OUT_FLACDECODER, d_out, d_info)
+                torch.cuda.synchronize()
+                if d_out.cpu().numpy()[: int(s.nsamples) * stride].tobytes() != oref:
+                    print(i, "FLACDecoder layout differs from the C# replay", flush=True)
+                    ok = False
         if ok and "--api" in sys.argv:  # libFLAC-compatible stream API events == the oracle's
             from birdnest.audio_amd import harness
             hev, hpcm = harness.run(data, driver=0)
