@@ -135,6 +135,15 @@ def main():
                 if d_out.cpu().numpy()[: int(s.nsamples) * stride].tobytes() != oref:
                     print(i, "FLACDecoder layout differs from the C# replay", flush=True)
                     ok = False
+        if ok and "--reader" in sys.argv and kw["bps"] == 16:  # streaming reader == the C# CopyTo replay
+            orc, oref, omsg, _ = oracle.flacdecoder_copyto(data)
+            if orc == 0:
+                r = libflac.Reader(data, libflac.OUT_FLACDECODER, window_frames=int(rng.integers(1, 64)))
+                got = r.read_all(int(rng.choice([1000, 16384, 65536])))
+                r.close()
+                if got != oref:
+                    print(i, "reader differs from the C# replay", flush=True)
+                    ok = False
         if ok and "--api" in sys.argv:  # libFLAC-compatible stream API events == the oracle's
             from birdnest.audio_amd import harness
             hev, hpcm = harness.run(data, driver=0)
