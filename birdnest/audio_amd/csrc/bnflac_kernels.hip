@@ -738,7 +738,11 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     fi.crc8 = fi.crc16_calc = fi.crc16_read = fi.crc_ok = 0;
     fi.flags = 0;
     fi.pad_ = 0;
-    for (int c = 0; c < 8; c++) fi.sub_start[c] = 0;
+    /* sub_start is kept in registers and written by select chains: indexing fi.sub_start
+     * with the runtime channel would put the whole record in scratch */
+    uint32_t ss[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) ss[c] = 0;
     const uint64_t limit = nbytes * 8u;
     const uint64_t fbit = fi.frame_off * 8u;
     BR b;
@@ -754,14 +758,20 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
         fi.out_sample = out_sample_in ? out_sample_in[f] : sample - base_sample;
         uint32_t maxorder = 0;
         for (uint32_t ch = 0; ch < fi.channels; ch++) {
-            fi.sub_start[ch] = (uint32_t)(br_pos(b) - fbit);
+            const uint32_t here = (uint32_t)(br_pos(b) - fbit);
+#pragma unroll
+            for (int c = 0; c < 8; c++) ss[c] = (uint32_t)c == ch ? here : ss[c];
             if (ch + 1 == fi.channels) {
                 /* the last subframe is walked by k_decode; only peek at its type byte */
                 const uint32_t x = br_peek(b) >> 24;
                 if (!(x & 0x80u) && (x & 0x7Eu) >= 0x40u) maxorder = max(maxorder, ((x >> 1) & 31u) + 1u);
                 break;
             }
-            if (ablate & 16u) { fi.sub_start[ch + 1] = fi.sub_start[ch]; continue; }
+            if (ablate & 16u) {
+#pragma unroll
+                for (int c = 0; c < 8; c++) ss[c] = (uint32_t)c == ch + 1 ? here : ss[c];
+                continue;
+            }
             SubHdr h;
             int32_t err = -1;
             uint32_t bps = sub_bps(fi, ch);
@@ -785,6 +795,8 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
         else if (fi.channels == 2) fi.flags |= BNF_FL_ST;
     }
     fi.status = st;
+#pragma unroll
+    for (int c = 0; c < 8; c++) fi.sub_start[c] = ss[c];
     info[f] = fi;
 }
 
