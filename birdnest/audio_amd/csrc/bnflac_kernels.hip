@@ -1296,7 +1296,8 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
     int32_t *row = lds + lane;
     if (active) {
         bs = fi.blocksize;
-        br_seek(b, fi.frame_off * 8u + fi.sub_start[ch]);
+        /* read from HBM: indexing the local record by the runtime channel would spill it to scratch */
+        br_seek(b, fi.frame_off * 8u + info[f].sub_start[ch]);
         int32_t warm[MAXW], coef[MAXW]; /* orders above MAXW are rejected below */
         st = parse_subframe_head<true, MAXW>(b, sub_bps(fi, ch), bs, limit, h, warm, coef, err);
         if (st == BNF_ST_OK && h.type == T_LPC && h.order > MAXW) {
