@@ -715,13 +715,16 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 }
 
 /* ==================================================================== k_parse */
+#ifndef PARSE_RD
+#define PARSE_RD 8 /* ring slots per lane (8 KB of LDS per wave, 5 waves per SIMD); 4 slots: 8 waves but 3% slower */
+#endif
 /* One lane per candidate frame: header + cursor walk over subframes 0..C-2.  Also
  * flags frames with an LPC order above 8 (they go to k_decode<32>). */
 __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint64_t nbytes,
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
                                               uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate) {
-    __shared__ uint32_t ring[RING_MAX * RING_LANE_DW];
+    __shared__ uint32_t ring[PARSE_RD * RING_LANE_DW];
     const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
     bnf_frame_info fi;
@@ -746,7 +749,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     const uint64_t limit = nbytes * 8u;
     const uint64_t fbit = fi.frame_off * 8u;
     BR b;
-    br_init(b, words, nbytes, (lds_u32 *)ring, threadIdx.x, RING_MAX);
+    br_init(b, words, nbytes, (lds_u32 *)ring, threadIdx.x, PARSE_RD);
     uint32_t st = parse_header(b, fbit, limit, sp, fi);
     if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
     if (st == BNF_ST_OK) {
