@@ -1,29 +1,39 @@
 #!/usr/bin/env python3
-"""Benchmark: MI355X FLAC frame decode on BASELINE config C2 (one JSON line on rank 0).
+"""Benchmark: MI355X FLAC frame decode on the BASELINE.json configs (one JSON line on rank 0).
 
-Workload: batches of 1024 synthetic frames (44.1 kHz / 16-bit stereo, blocksize 4096,
-LPC order 8, Rice partition order 4), the compressed frames resident in HBM.  One step
-decodes ``--batches`` independent batches (distinct copies in HBM, so nothing is served
-from a previous step's cache footprint) into FLACDecoder's 16-bit interleaved LE PCM
-(the OpenAL buffer-fill layout, FLACDecoder.cs:543-562) with the two kernels of the
-path, k_parse and k_decode, on one HIP stream.
+Headline (`--config C2`, the default): batches of 1024 synthetic frames (44.1 kHz / 16-bit
+stereo, blocksize 4096, LPC order 8, Rice partition order 4), compressed frames resident in
+HBM.  One step decodes ``--batches`` independent copies (distinct HBM regions, so nothing is
+served from a previous step's cache footprint) into FLACDecoder's 16-bit interleaved LE PCM
+(the OpenAL buffer-fill layout, FLACDecoder.cs:543-562) with the two launches of the path,
+k_parse and the decode launch (k_decode_st + k_decode<8|32>), on one HIP stream.
 
-value      = decoded samples (blocksize x channels) per second,
-             whole job over all ranks (weak scaling: every rank decodes its own batches).
-roofline   = the dominant kernel (k_decode): algorithmic bytes (compressed frame bytes +
-             PCM bytes written) / its HIP-event-timed average duration, vs 8 TB/s HBM.
-cpu_baseline = the CPU restatement (oracle/: libFLAC 1.2.1 decode + FLACDecoder pack) on
-             min(16, cpu count) threads, plus a 1-thread figure, on a bounded sample of
-             the same frames.
-Beside the metric (rank 0): indexer (bnflac_index_stream over one stream), reader
-(bnflac_reader_* from host bytes to 16 KiB reads), pcie_inclusive (host-resident batches).
+The other 1-GPU configs are side legs of the same line (rank 0, N = 1 only; `--legs`):
+  C3  96 kHz/24-bit stereo, LPC-12, bs 8192, wasted bits + mid/side -> FLACFileReader 3-byte PCM
+  C4  mixed CONSTANT/VERBATIM/FIXED/LPC, variable bs 192-16384, 16-bit stereo -> FLACDecoder PCM
+  C5  192 kHz/24-bit 8-channel LPC-32 files (469 frames each) -> FLACFileReader 3-byte PCM
+Each leg reports value, the decode launch's roofline, a step-level roofline and its own
+cpu_baseline.  `--config C5` makes C5 the headline: 8 files sharded over the ranks
+(shard.partition), each rank indexing its files on the GPU (bnflac_index_stream) and decoding
+them, then the interleaved PCM gathered to rank 0 over RCCL (shard.gather_bytes, concurrent
+point-to-point receives); decode-only and decode+gather times are reported separately.
 
-    python bench.py [--gpus N --steps K --warmup W --batches B]
+value        = decoded samples (blocksize x channels) per second, whole
+               job over all ranks (weak scaling for C2-C4: every rank decodes its own batches).
+roofline     = the dominant launch (the decode launch): algorithmic bytes (compressed frame bytes +
+               PCM bytes written) / its HIP-event-timed average duration on the stream it
+               runs on, vs 8 TB/s HBM; step_frac = the same bytes / the whole step (k_parse included).
+cpu_baseline = the CPU restatement (oracle/: libFLAC 1.2.1 decode + the C# pack of the config) on
+               every host core this process may use (os.sched_getaffinity), plus a 1-thread figure,
+               on a bounded sample of the same frames.
+
+    python bench.py [--gpus N --steps K --warmup W --batches B --config C2|C3|C4|C5 --legs C3,C4,C5]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -37,22 +47,41 @@ sys.path.insert(0, ROOT)
 METRIC = "decoded PCM MSamples/s/GPU (bit-exact) + achieved HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
+# per config: output layout of the reference's C# surface for it, default copies per step,
+# and what the config is (BASELINE.json configs[1..4])
+CONFIGS = {
+    "C2": dict(fmt="FLACDECODER", batches=1024, frames=1024,
+               desc="C2: 1024-frame batches, 44.1 kHz/16-bit stereo, bs 4096, LPC-8, Rice partition order 4 "
+                    "-> FLACDecoder 16-bit LE interleaved PCM"),
+    "C3": dict(fmt="FILEREADER", batches=64, frames=1024,
+               desc="C3: 1024-frame batches, 96 kHz/24-bit stereo, LPC-12, bs 8192, wasted bits + mid/side "
+                    "-> FLACFileReader 24-bit LE interleaved PCM"),
+    "C4": dict(fmt="FLACDECODER", batches=32, frames=4096,
+               desc="C4: 4096-frame mixed corpus (CONSTANT/VERBATIM/FIXED/LPC, variable bs 192-16384), "
+                    "16-bit stereo -> FLACDecoder 16-bit LE interleaved PCM"),
+    "C5": dict(fmt="FILEREADER", batches=8, frames=469,
+               desc="C5: 10 s files, 192 kHz/24-bit 8-channel, LPC-32, bs 4096 -> FLACFileReader 24-bit LE "
+                    "interleaved PCM"),
+}
+
 
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batches", type=int, default=1024,
-                    help="C2 batches (x1024 frames) decoded per step; 128 = one k_decode_st wave (64 frames) "
-                         "per resident slot (256 CUs x 8 waves); 1024 = eight such rounds (DESIGN.md section 5)")
-    ap.add_argument("--frames", type=int, default=1024, help="frames per batch (BASELINE C2: 1024)")
-    ap.add_argument("--groups", type=int, default=1,
-                    help="pipeline groups: k_parse of group g+1 overlaps k_decode of group g (1 = serial)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS), help="headline workload")
+    ap.add_argument("--batches", type=int, default=0,
+                    help="copies decoded per step (0: the config's default; C2: 1024 = eight rounds of "
+                         "k_decode_st waves, DESIGN.md section 5; C5: files in the job)")
+    ap.add_argument("--frames", type=int, default=0, help="frames per batch (0: the config's)")
+    ap.add_argument("--legs", default="C3,C4,C5", help="side legs at N = 1 (comma list, '' for none)")
+    ap.add_argument("--leg-steps", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (headline)")
+    ap.add_argument("--leg-cpu-seconds", type=float, default=3.0, help="CPU baseline time budget per leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="host threads for the multi-thread CPU baseline (0: min(16, cpu count))")
+                    help="host threads for the multi-thread CPU baseline (0: every core in the affinity mask)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-resident) measurement")
     ap.add_argument("--no-index", action="store_true", help="skip the frame-indexer (bnflac_index_stream) timing")
     ap.add_argument("--no-reader", action="store_true", help="skip the streaming-reader (bnflac_reader_*) timing")
@@ -64,46 +93,19 @@ def parse_args():
     return ap.parse_args()
 
 
-def cpu_baseline(data: bytes, nsamples_per_pass: int, budget_s: float, threads: int = 1):
-    """Oracle (restated libFLAC 1.2.1 + FLACDecoder.CopyTo pack) on `threads` host threads,
-    each decoding whole batches independently (a libFLAC decoder is single-threaded per
-    stream; ctypes releases the GIL during the call)."""
-    import threading
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    oracle.lib()
-    counts = [0] * threads
-    t0 = time.perf_counter()
-
-    def run(i):
-        while time.perf_counter() - t0 < budget_s:
-            rc, pk, msg, _ = oracle.flacdecoder_copyto(data)
-            assert rc == 0, msg
-            counts[i] += 1
-
-    ths = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    el = time.perf_counter() - t0
-    passes = sum(counts)
-    return passes * nsamples_per_pass / el / 1e6, passes, el
+def affinity_cores() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
-def measured_traffic(B: int, frames: int, G: int):
-    """HBM bytes per k_decode launch from a committed PMC summary of this same workload
-    (profiles/traffic_c2_b<B>.json, written from tools/pmc_session.sh counters with the
-    MI355X_MICROARCH.md corrections).  PMC counters cannot be read from inside this run;
-    None when no summary matches the configuration."""
-    path = os.path.join(ROOT, "profiles", f"traffic_c2_b{B}.json")
-    if G != 1 or not os.path.exists(path):
-        return None
-    d = json.load(open(path))
-    if d.get("batches_per_step") != B or d.get("frames_per_batch") != frames:
-        return None
-    return {"traffic_bytes": int(d["traffic_bytes"]),
-            "source": f"profiles/{os.path.basename(path)} ({d.get('round', '?')}: FETCH_SIZE x2 + WRITE_SIZE)"}
+def host_threads() -> int:
+    """Every core this process may use, capped by the box's CPU share for one GPU when the
+    environment states one (OMP_NUM_THREADS: the GPU box sets it to its share)."""
+    n = affinity_cores()
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(share)) if share.isdigit() and int(share) > 0 else n
 
 
 def cpu_model() -> str:
@@ -116,29 +118,236 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def pcie_inclusive(args, torch, dev, libflac, dec, data, offs, sp, p, s, pcm_bytes, samples_per_batch, nb=8, reps=3):
+def kernels_sha() -> str:
+    """Hash of the kernel/runtime sources the timed library was built from (ties a committed
+    PMC traffic summary to this build)."""
+    h = hashlib.sha256()
+    for f in ("bnflac_kernels.hip", "bnflac_device.h", "bnflac_runtime.cpp"):
+        h.update(open(os.path.join(ROOT, "birdnest", "audio_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pack_reference(pcm: np.ndarray, fmt: str, bps: int) -> bytes:
+    """Expected bytes of the lossless round trip in the C# layout (generator PCM is the golden)."""
+    if fmt == "FLACDECODER":
+        return pcm.astype("<i2").tobytes()
+    if bps == 16:
+        return pcm.astype("<i2").tobytes()
+    return np.ascontiguousarray(pcm.astype("<i4")).view(np.uint8).reshape(-1, 4)[:, :3].tobytes()
+
+
+class Workload:
+    """B copies of one synthetic stream's frames resident in HBM, with their records and output."""
+
+    def __init__(self, cfg, B, frames, torch, dev, libflac, synth, dec, seed=None):
+        c = CONFIGS[cfg]
+        self.cfg, self.B = cfg, B
+        kw = {"nframes": frames or c["frames"]}
+        if seed is not None:
+            kw["seed"] = seed
+        p = synth.config(cfg, **kw)
+        if kw["nframes"] != CONFIGS[cfg]["frames"] and p.last_blocksize:
+            p.last_blocksize = 0
+        s = synth.encode(p)
+        self.p, self.s = p, s
+        self.data = s.data.tobytes()
+        self.offs = s.frame_offsets.astype(np.int64)
+        self.nf1 = len(self.offs)
+        self.fb_in = int(len(self.data) - self.offs[0])          # compressed frame bytes (sync .. CRC-16)
+        self.samples1 = int(s.nsamples) * p.channels
+        self.fmt_name = c["fmt"]
+        self.fmt = getattr(libflac, "OUT_" + c["fmt"])
+        self.sp = libflac.StreamParams.from_synth(p, s.nsamples)
+        self.stride = libflac.out_stride(self.fmt, self.sp)
+        self.pcm1 = int(s.nsamples) * self.stride
+        self.ref = pack_reference(s.pcm, c["fmt"], p.bps)
+        assert len(self.ref) == self.pcm1
+        self.torch, self.dev, self.libflac, self.dec = torch, dev, libflac, dec
+        copy_len = (len(self.data) + 255) // 256 * 256
+        self.copy_len = copy_len
+        one = np.zeros(copy_len, dtype=np.uint8)
+        one[:len(self.data)] = np.frombuffer(self.data, dtype=np.uint8)
+        self.d_bytes = torch.zeros(copy_len * B + 64, dtype=torch.uint8, device=dev)
+        self.d_bytes[:copy_len * B].view(B, copy_len).copy_(torch.from_numpy(one).to(dev).unsqueeze(0).expand(B, copy_len))
+        self.nbytes = copy_len * B
+        # frame positions of copy 0 from the headers (variable blocksizes: sample numbers)
+        d_o1 = torch.from_numpy(self.offs).to(dev)
+        d_i1 = torch.zeros(self.nf1 * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+        dec.parse_frames(self.d_bytes, copy_len, d_o1, self.nf1, self.sp, d_i1)
+        torch.cuda.synchronize(dev)
+        inf = libflac.info_array(d_i1.cpu().numpy())
+        assert (inf["status"] == 0).all(), "k_parse rejected a generated frame"
+        fr_start = inf["out_sample"].astype(np.int64)
+        self.nframes = self.nf1 * B
+        self.d_offs = torch.from_numpy(np.concatenate([self.offs + b * copy_len for b in range(B)])).to(dev)
+        self.d_os = torch.from_numpy(np.concatenate([fr_start + b * int(s.nsamples) for b in range(B)])).to(dev)
+        self.d_out = torch.empty(self.pcm1 * B, dtype=torch.uint8, device=dev)
+        self.d_info = torch.zeros(self.nframes * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+        self.alg_bytes = (self.fb_in + self.pcm1) * B       # per decode launch
+        self.samples = self.samples1 * B                     # per step
+
+    def parse(self, stream):
+        self.dec.parse_frames(self.d_bytes, self.nbytes, self.d_offs, self.nframes, self.sp, self.d_info,
+                              d_out_sample=self.d_os, stream=stream)
+
+    def decode(self, stream):
+        self.dec.decode_parsed(self.d_bytes, self.nbytes, self.nframes, self.sp, self.fmt, self.d_out, self.d_info,
+                               stream=stream)
+
+    def run(self, K, stream, pev=None, dev_ev=None):
+        torch = self.torch
+        for _ in range(K):
+            if pev is not None:
+                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                e[0].record(stream)
+                self.parse(stream)
+                e[1].record(stream)
+                pev.append(e)
+            else:
+                self.parse(stream)
+            if dev_ev is not None:
+                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                e[0].record(stream)
+                self.decode(stream)
+                e[1].record(stream)
+                dev_ev.append(e)
+            else:
+                self.decode(stream)
+
+    def check(self) -> bool:
+        """Every frame ok (sampled records) and copies 0 and B-1 equal the source PCM."""
+        lf = self.libflac
+        info = lf.info_array(self.d_info.view(-1, lf.FRAME_INFO_BYTES)[:: max(1, self.nframes // 4096)].cpu().numpy())
+        ok = bool((info["status"] == 0).all() and (info["crc_ok"] == 1).all())
+        for b in sorted({0, self.B - 1}):
+            got = self.d_out[b * self.pcm1:(b + 1) * self.pcm1].cpu().numpy().tobytes()
+            ok = ok and got == self.ref
+        return ok
+
+
+def timed(wl, steps, warmup, stream, world, dist, dev):
+    """warmup, then K timed steps between barriers + device syncs; returns elapsed (max over
+    ranks), k_parse and decode-launch averages (ms, HIP events on the launch stream)."""
+    torch = wl.torch
+    wl.run(warmup, stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    pev, dev_ev = [], []
+    t0 = time.perf_counter()
+    wl.run(steps, stream, pev, dev_ev)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_parse = sum(a.elapsed_time(b) for a, b in pev) / len(pev)
+    t_decode = sum(a.elapsed_time(b) for a, b in dev_ev) / len(dev_ev)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, t_parse, t_decode
+
+
+def roofline(alg_bytes, t_decode_ms, t_parse_ms, step_ms, traffic=None):
+    achieved = alg_bytes / (t_decode_ms * 1e-3) / 1e9
+    step = alg_bytes / (step_ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "kernel": "decode launch (k_decode_st + k_decode<8> + k_decode<32>)",
+         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+         "traffic": None, "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(t_decode_ms, 4),
+         "k_parse_avg_ms": round(t_parse_ms, 4), "step_achieved_GBs": round(step, 1),
+         "step_frac": round(step / HBM_PEAK_GBS, 4)}
+    if traffic is not None:
+        r["traffic"] = traffic["traffic_bytes"]
+        r["traffic_over_alg"] = round(traffic["traffic_bytes"] / alg_bytes, 3)
+        r["traffic_source"] = traffic["source"]
+    return r
+
+
+def measured_traffic(cfg: str, B: int, frames: int):
+    """HBM bytes per decode launch from a committed PMC summary of this workload AND this build
+    (profiles/traffic_<cfg>_b<B>.json from tools/pmc_session.sh + tools/pmc_summary.py, with the
+    MI355X_MICROARCH.md FETCH_SIZE correction).  Counters cannot be read inside the timed run;
+    None when no summary matches the workload and the kernel sources' hash."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{cfg.lower()}_b{B}.json")
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    if d.get("batches_per_step") != B or d.get("frames_per_batch") != frames or d.get("kernels_sha") != kernels_sha():
+        return None
+    return {"traffic_bytes": int(d["traffic_bytes"]),
+            "source": f"profiles/{os.path.basename(path)} ({d.get('round', '?')}, kernels {d['kernels_sha']}: "
+                      f"FETCH_SIZE x2 + WRITE_SIZE)"}
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(data: bytes, fmt: str, buf_len: int, samples_per_pass: int, budget_s: float, threads: int):
+    """The oracle (restated libFLAC 1.2.1 + the C# pack of the layout) on `threads` host threads,
+    each decoding whole streams independently (a libFLAC decoder is single-threaded per stream;
+    ctypes releases the GIL during the call)."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.lib()
+    counts = [0] * threads
+    t0 = time.perf_counter()
+
+    def run(i):
+        while time.perf_counter() - t0 < budget_s:
+            if fmt == "FLACDECODER":
+                rc, _, msg, _ = oracle.flacdecoder_copyto(data)
+            else:
+                rc, _, msg = oracle.filereader_readall(data, buf_len=buf_len)
+            assert rc == 0, msg
+            counts[i] += 1
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    passes = sum(counts)
+    return passes * samples_per_pass / el / 1e6, passes, el
+
+
+def cpu_leg(wl, budget_s, threads_arg):
+    nthr = threads_arg or host_threads()
+    p = wl.p
+    buf_len = p.blocksize * p.channels * (3 if p.bps == 24 else 2)  # one frame per FLACFileReader.Read
+    what = "FLACDecoder.CopyTo replay" if wl.fmt_name == "FLACDECODER" else f"FLACFileReader.Read replay ({buf_len} B reads)"
+    mss1, passes1, el1 = cpu_baseline(wl.data, wl.fmt_name, buf_len, wl.samples1, max(1.0, budget_s / 4), 1)
+    mss, passes, el = cpu_baseline(wl.data, wl.fmt_name, buf_len, wl.samples1, budget_s, nthr)
+    return {"value": round(mss, 3), "unit": "MSamples/s", "cores": nthr, "kind": "port",
+            "cores_note": f"threads = the host cores available to this process: affinity mask {affinity_cores()}, "
+                          f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')} (the box's CPU share per GPU)",
+            "sample": f"{passes} x one {wl.cfg} stream ({wl.nf1} frames, {wl.samples1} samples) through the oracle's "
+                      f"{what} on {nthr} threads, {el:.1f} s",
+            "single_thread": {"value": round(mss1, 3), "cores": 1, "passes": passes1, "seconds": round(el1, 2)},
+            "cpu": cpu_model()}
+
+
+# --------------------------------------------------------------------------- side measurements
+def pcie_inclusive(wl, nb=8, reps=3):
     """Host-resident caller: pinned host compressed bytes -> H2D -> parse+decode -> D2H PCM.
     Reported beside `value`, never as it."""
-    copy_len = (len(data) + 255) // 256 * 256
+    torch, dev, lf, dec = wl.torch, wl.dev, wl.libflac, wl.dec
+    nb = min(nb, wl.B)
+    copy_len = wl.copy_len
     h_in = torch.zeros(copy_len * nb + 64, dtype=torch.uint8).pin_memory()
-    src = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy())
-    for b in range(nb):
-        h_in[b * copy_len: b * copy_len + len(data)] = src
-    h_out = torch.empty(pcm_bytes * nb, dtype=torch.uint8).pin_memory()
+    h_in[:copy_len * nb].copy_(wl.d_bytes[:copy_len * nb].cpu())
+    h_out = torch.empty(wl.pcm1 * nb, dtype=torch.uint8).pin_memory()
     d_in = torch.empty_like(h_in, device=dev)
-    d_out = torch.empty(pcm_bytes * nb, dtype=torch.uint8, device=dev)
-    d_offs = torch.from_numpy(np.concatenate([offs + b * copy_len for b in range(nb)])).to(dev)
-    fr_bs = np.full(args.frames, p.blocksize, dtype=np.int64)
-    fr_start = np.concatenate([[0], np.cumsum(fr_bs)[:-1]])
-    d_os = torch.from_numpy(np.concatenate([fr_start + b * int(s.nsamples) for b in range(nb)])).to(dev)
-    nf = args.frames * nb
-    d_info = torch.zeros(nf * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(wl.pcm1 * nb, dtype=torch.uint8, device=dev)
+    nf = wl.nf1 * nb
+    d_info = torch.zeros(nf * lf.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     def once():
         d_in.copy_(h_in, non_blocking=True)
-        dec.decode_frames(d_in, copy_len * nb, d_offs, nf, sp, libflac.OUT_FLACDECODER, d_out, d_info,
-                          d_out_sample=d_os, stream=stream)
+        dec.decode_frames(d_in, copy_len * nb, wl.d_offs[:nf], nf, wl.sp, wl.fmt, d_out, d_info,
+                          d_out_sample=wl.d_os[:nf], stream=stream)
         h_out.copy_(d_out, non_blocking=True)
 
     once()
@@ -148,50 +357,169 @@ def pcie_inclusive(args, torch, dev, libflac, dec, data, offs, sp, p, s, pcm_byt
         once()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    ok = h_out[:pcm_bytes].numpy().tobytes() == s.pcm.astype("<i2").tobytes()
-    return {"value": round(samples_per_batch * nb * reps / el / 1e6, 2), "unit": "MSamples/s",
+    ok = h_out[:wl.pcm1].numpy().tobytes() == wl.ref
+    return {"value": round(wl.samples1 * nb * reps / el / 1e6, 2), "unit": "MSamples/s",
             "batches": nb * reps, "bitexact": bool(ok),
-            "note": "pinned host bytes -> H2D -> k_parse+k_decode -> D2H PCM, serialized on one stream"}
+            "note": "pinned host bytes -> H2D -> k_parse+decode -> D2H PCM, serialized on one stream"}
 
 
-def index_leg(torch, dev, libflac, dec, data, offs, sp, reps=5):
-    """bnflac_index_stream over one whole C2 stream in HBM: sync scan,
-    candidate parse, CRC-16 chain.  Wall time per call (it syncs once for the candidate
-    count).  Reported beside `value`, not part of it."""
-    n = len(data)
+def index_leg(wl, reps=5):
+    """bnflac_index_stream over one whole stream in HBM: sync scan, candidate
+    parse, CRC-16 chain.  Wall time per call (it syncs once for the candidate count)."""
+    torch, dev, dec = wl.torch, wl.dev, wl.dec
+    n = len(wl.data)
     d = torch.zeros((n + 15) // 16 * 16 + 16, dtype=torch.uint8, device=dev)
-    d[:n] = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).to(dev)
-    cap = len(offs) + 16
-    o, _, _, nf = dec.index_stream(d, n, int(offs[0]), sp, cap)
-    match = nf == len(offs) and bool(np.array_equal(o[:nf].cpu().numpy(), offs))
+    d[:n] = torch.from_numpy(np.frombuffer(wl.data, dtype=np.uint8).copy()).to(dev)
+    cap = len(wl.offs) + 16
+    o, _, _, nf = dec.index_stream(d, n, int(wl.offs[0]), wl.sp, cap)
+    match = nf == len(wl.offs) and bool(np.array_equal(o[:nf].cpu().numpy(), wl.offs))
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(reps):
-        dec.index_stream(d, n, int(offs[0]), sp, cap)
+        dec.index_stream(d, n, int(wl.offs[0]), wl.sp, cap)
     ms = (time.perf_counter() - t0) / reps * 1e3
     return {"ms": round(ms, 4), "GB_per_s": round(n / (ms * 1e-3) / 1e9, 2), "frames": nf, "stream_bytes": n,
             "matches_generator_offsets": match,
-            "note": "one C2 stream: sync scan + k_parse of every candidate + CRC-16 chain (one host sync)"}
+            "note": "one stream: sync scan + k_parse of every candidate + CRC-16 chain (one host sync)"}
 
 
-def reader_leg(libflac, data, pcm_ref: bytes, samples: int, reps=3, chunk=16384):
-    """bnflac_reader over one whole C2 stream held in host memory: open
-    (H2D, frame index, decode-ahead) + Read() in OpenAL-sized 16 KiB pieces until the end.
-    Host-link and Python-call bound; reported beside `value`, not part of it."""
+def reader_leg(wl, reps=3, chunk=16384):
+    """bnflac_reader over one whole stream held in host memory: open (H2D, frame
+    index, decode-ahead) + Read() in OpenAL-sized 16 KiB pieces until the end.  Reported beside
+    `value`, not part of it."""
+    lf = wl.libflac
     best, ok = None, True
     for _ in range(reps):
         t0 = time.perf_counter()
-        r = libflac.Reader(data, libflac.OUT_FLACDECODER)
+        r = lf.Reader(wl.data, wl.fmt)
         got = r.read_all(chunk)
         r.close()
         el = time.perf_counter() - t0
-        ok = ok and got == pcm_ref
+        ok = ok and got == wl.ref
         best = el if best is None else min(best, el)
-    return {"value": round(samples / best / 1e6, 2), "unit": "MSamples/s", "ms": round(best * 1e3, 2),
+    return {"value": round(wl.samples1 / best / 1e6, 2), "unit": "MSamples/s", "ms": round(best * 1e3, 2),
             "bitexact": bool(ok), "read_bytes": chunk,
             "note": "host bytes -> bnflac_reader_open (H2D, index, decode-ahead) -> Read() x 16 KiB until EOS"}
 
 
+def leg(cfg, args, torch, dev, libflac, synth, dec, stream):
+    """One side config on this GPU: value, decode-launch roofline, step roofline, cpu_baseline."""
+    c = CONFIGS[cfg]
+    wl = Workload(cfg, c["batches"], 0, torch, dev, libflac, synth, dec)
+    el, tp, td = timed(wl, args.leg_steps, 1, stream, 1, None, dev)
+    ok = wl.check()
+    step_ms = el / args.leg_steps * 1e3
+    out = {"value": round(wl.samples * args.leg_steps / el / 1e6, 2), "unit": "MSamples/s",
+           "ms_per_step": round(step_ms, 4), "steps": args.leg_steps, "bitexact": ok,
+           "config": {"workload": c["desc"], "frames_per_batch": wl.nf1, "batches_per_step": wl.B,
+                      "compressed_bytes_per_batch": wl.fb_in, "pcm_bytes_per_batch": wl.pcm1},
+           "roofline": roofline(wl.alg_bytes, td, tp, step_ms, measured_traffic(cfg, wl.B, wl.nf1))}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_leg(wl, args.leg_cpu_seconds, args.cpu_threads)
+    del wl
+    torch.cuda.empty_cache()
+    return out
+
+
+# --------------------------------------------------------------------------- C5: files over ranks
+def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
+    """C5 as BASELINE.json states it: F files of 192 kHz/24-bit 8-channel LPC-32 audio sharded
+    over the ranks (shard.partition by samples), each rank indexing its files on the GPU
+    (bnflac_index_stream, untimed setup) and decoding them (timed: k_parse + decode launch over
+    all its files at once), then the FLACFileReader PCM gathered to rank 0 (shard.gather_bytes:
+    concurrent RCCL receives over xGMI)."""
+    from birdnest.audio_amd import shard
+    F = args.batches or CONFIGS["C5"]["batches"]
+    p0 = synth.config("C5")
+    ranges = shard.partition([p0.nframes * p0.blocksize] * F, world)  # equal files: F/world each
+    lo, hi = ranges[rank]
+    mine = list(range(lo, hi))
+    streams = [synth.encode(synth.config("C5", seed=5 + 1000 * i)) for i in mine]
+    sp = libflac.StreamParams.from_synth(p0, streams[0].nsamples if streams else 0)
+    fmt = libflac.OUT_FILEREADER
+    stride = libflac.out_stride(fmt, sp)
+    lens = [(len(s.data) + 255) // 256 * 256 for s in streams]
+    base = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) if streams else np.zeros(1, np.int64)
+    d_bytes = torch.zeros(int(base[-1]) + 64, dtype=torch.uint8, device=dev)
+    offs, osmp, nsmp = [], [], 0
+    for i, s in enumerate(streams):
+        n = len(s.data)
+        d_bytes[int(base[i]):int(base[i]) + n] = torch.from_numpy(s.data.copy()).to(dev)
+        o, os_, _, nf = dec.index_stream(d_bytes[int(base[i]):], n, int(s.frame_offsets[0]), sp, len(s.frame_offsets) + 8)
+        assert nf == len(s.frame_offsets), "GPU frame index disagrees with the generator"
+        offs.append(o[:nf].cpu().numpy() + int(base[i]))
+        osmp.append(os_[:nf].cpu().numpy() + nsmp)
+        nsmp += s.nsamples
+    nframes = int(sum(len(o) for o in offs))
+    d_offs = torch.from_numpy(np.concatenate(offs) if offs else np.zeros(0, np.int64)).to(dev)
+    d_os = torch.from_numpy(np.concatenate(osmp) if osmp else np.zeros(0, np.int64)).to(dev)
+    d_out = torch.empty(max(nsmp * stride, 1), dtype=torch.uint8, device=dev)
+    d_info = torch.zeros(max(nframes, 1) * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    nb = int(base[-1])
+
+    def decode():
+        if nframes:
+            dec.parse_frames(d_bytes, nb, d_offs, nframes, sp, d_info, d_out_sample=d_os, stream=stream)
+            dec.decode_parsed(d_bytes, nb, nframes, sp, fmt, d_out, d_info, stream=stream)
+
+    for _ in range(args.warmup):
+        decode()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ev = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        e[0].record(stream)
+        decode()
+        e[1].record(stream)
+        ev.append(e)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t_dec = time.perf_counter() - t0
+    t_launch = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    # decode + gather: the same steps, each followed by the gather of every rank's PCM to rank 0
+    gathered = None
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        decode()
+        if world > 1:
+            gathered = shard.gather_bytes(d_out[:nsmp * stride])
+        else:
+            gathered = d_out[:nsmp * stride]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t_all = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([t_dec, t_all], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_dec, t_all = float(t[0].item()), float(t[1].item())
+    ok = True
+    if rank == 0:
+        local = dict(zip(mine, streams))
+        ref = b"".join(pack_reference((local[i] if i in local else synth.encode(synth.config("C5", seed=5 + 1000 * i))).pcm,
+                                      "FILEREADER", 24) for i in range(F))
+        ok = gathered is not None and gathered.cpu().numpy().tobytes() == ref
+    if world > 1:
+        o = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(o, op=dist.ReduceOp.MIN)
+        ok = bool(o.item())
+    samples = sum(s.nsamples for s in streams) * p0.channels
+    tot = torch.tensor([samples], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    samples = int(tot.item())
+    comp = sum(len(s.data) - int(s.frame_offsets[0]) for s in streams)
+    alg = comp + nsmp * stride
+    return {"samples": samples, "t_dec": t_dec, "t_all": t_all, "t_launch": t_launch, "ok": ok, "files": F,
+            "alg_bytes_rank": alg, "frames_rank": nframes}
+
+
+# --------------------------------------------------------------------------- main
 def main():
     args = parse_args()
     import torch
@@ -208,125 +536,48 @@ def main():
     torch.cuda.set_device(dev)
 
     from birdnest.audio_amd import libflac, synth
-    p = synth.config("C2", nframes=args.frames, seed=2)
-    s = synth.encode(p)
-    data = s.data.tobytes()
-    offs = s.frame_offsets.astype(np.int64)
-    fb_in = int(len(data) - offs[0])               # compressed frame bytes (sync .. CRC-16)
-    samples_per_batch = int(s.nsamples) * p.channels
-    sp = libflac.StreamParams.from_synth(p, s.nsamples)
-    stride = libflac.out_stride(libflac.OUT_FLACDECODER, sp)
-    pcm_bytes_per_batch = int(s.nsamples) * stride
-    B = args.batches
-
-    # B distinct copies of the batch in HBM (4-byte aligned), one output region each
-    copy_len = (len(data) + 255) // 256 * 256
-    one = np.zeros(copy_len, dtype=np.uint8)
-    one[:len(data)] = np.frombuffer(data, dtype=np.uint8)
-    d_bytes = torch.zeros(copy_len * B + 64, dtype=torch.uint8, device=dev)
-    d_bytes[:copy_len * B].view(B, copy_len).copy_(torch.from_numpy(one).to(dev).unsqueeze(0).expand(B, copy_len))
-    nbytes_total = copy_len * B
-    d_offs = torch.from_numpy(np.concatenate([offs + b * copy_len for b in range(B)])).to(dev)
-    nframes = args.frames * B
-    fr_bs = np.full(args.frames, p.blocksize, dtype=np.int64)
-    fr_start = np.concatenate([[0], np.cumsum(fr_bs)[:-1]])
-    d_out_sample = torch.from_numpy(np.concatenate([fr_start + b * int(s.nsamples) for b in range(B)])).to(dev)
-    d_out = torch.empty(pcm_bytes_per_batch * B, dtype=torch.uint8, device=dev)
-    d_info = torch.zeros(nframes * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
     dec = libflac.BatchDecoder(local_rank)
     stream = torch.cuda.current_stream(dev)
+    cfg = args.config
+    c = CONFIGS[cfg]
 
-    # Pipelined schedule: B batches in G groups; k_parse of the next group (stream sP)
-    # overlaps k_decode of the current one (stream sD).  Every timed step decodes all B
-    # batches; the pipeline fill (first parse) is inside the timed region.
-    G = args.groups
-    if B % G:
-        raise SystemExit("--batches must be a multiple of --groups")
-    nf_g = nframes // G
-    FIB = libflac.FRAME_INFO_BYTES
-    sP = torch.cuda.Stream(dev)
-    sD = torch.cuda.Stream(dev)
-    ev_parsed = [torch.cuda.Event() for _ in range(G)]
-    ev_decoded = [torch.cuda.Event() for _ in range(G)]
-    views = [(d_offs[g * nf_g:(g + 1) * nf_g], d_out_sample[g * nf_g:(g + 1) * nf_g],
-              d_info[g * nf_g * FIB:(g + 1) * nf_g * FIB]) for g in range(G)]
+    if cfg == "C5":
+        r = c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank)
+        step_ms = r["t_dec"] / args.steps * 1e3
+        line = {
+            "metric": METRIC, "value": round(r["samples"] * args.steps / r["t_dec"] / 1e6, 2), "unit": "MSamples/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_ms, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic: deterministic generator (seeds 5 + 1000 i), BASELINE C5 file shape",
+            "config": {"workload": c["desc"] + f"; {r['files']} files sharded over {world} rank(s), "
+                                                "decode-only timing (gather reported beside it)",
+                       "files": r["files"], "parallelism": f"files sharded per rank x{world} + RCCL gather to rank 0"},
+            "bitexact": r["ok"],
+            "roofline": roofline(r["alg_bytes_rank"], r["t_launch"], 0.0, step_ms),
+            "with_gather": {"value": round(r["samples"] * args.steps / r["t_all"] / 1e6, 2), "unit": "MSamples/s",
+                            "ms_per_step": round(r["t_all"] / args.steps * 1e3, 4),
+                            "note": "each step: decode, then shard.gather_bytes of every rank's PCM to rank 0"},
+        }
+        line["roofline"]["kernel"] = "k_parse + decode launch over the rank's files"
+        if rank == 0:
+            js = json.dumps(line)
+            print(js, flush=True)
+            if args.out:
+                open(args.out, "w").write(js + "\n")
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
-    def parse(g, tev=None):
-        sP.wait_event(ev_decoded[g])  # the group's frame records are free again
-        if tev is not None:
-            tev[0].record(sP)
-        o, osmp, inf = views[g]
-        dec.parse_frames(d_bytes, nbytes_total, o, nf_g, sp, inf, d_out_sample=osmp, stream=sP)
-        if tev is not None:
-            tev[1].record(sP)
-        ev_parsed[g].record(sP)
-
-    def decode(g, tev=None):
-        sD.wait_event(ev_parsed[g])
-        if tev is not None:
-            tev[0].record(sD)
-        dec.decode_parsed(d_bytes, nbytes_total, nf_g, sp, libflac.OUT_FLACDECODER, d_out, views[g][2], stream=sD)
-        if tev is not None:
-            tev[1].record(sD)
-        ev_decoded[g].record(sD)
-
-    def run(K, pev=None, dev_=None):
-        """K full steps; pev/dev_: per-launch timing event pairs (lists, appended to)."""
-        def te(lst):
-            if lst is None:
-                return None
-            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            lst.append(e)
-            return e
-        parse(0, te(pev))
-        for k in range(K):
-            for g in range(G):
-                decode(g, te(dev_))
-                if g + 1 < G:
-                    parse(g + 1, te(pev))
-                elif k + 1 < K:
-                    parse(0, te(pev))
-
-    run(args.warmup)
-    torch.cuda.synchronize(dev)
-    pev, dev_ev = [], []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run(args.steps, pev, dev_ev)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t_parse = sum(a.elapsed_time(b) for a, b in pev) / len(pev)  # ms per k_parse launch (one group)
-    t_decode = sum(a.elapsed_time(b) for a, b in dev_ev) / len(dev_ev)  # ms per k_decode launch (one group)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    def step():  # one serial step on the default stream (stats / ablation timing)
-        dec.parse_frames(d_bytes, nbytes_total, d_offs, nframes, sp, d_info, d_out_sample=d_out_sample, stream=stream)
-        dec.decode_parsed(d_bytes, nbytes_total, nframes, sp, libflac.OUT_FLACDECODER, d_out, d_info, stream=stream)
-
-    # correctness of what was timed: every frame ok, copies 0 and B-1 == source PCM
-    info = libflac.info_array(d_info.view(-1, libflac.FRAME_INFO_BYTES)[:: max(1, nframes // 4096)].cpu().numpy())
-    ok = bool((info["status"] == 0).all() and (info["crc_ok"] == 1).all())
-    ref = s.pcm.astype("<i2").tobytes()
-    for b in {0, B - 1}:
-        got = d_out[b * pcm_bytes_per_batch:(b + 1) * pcm_bytes_per_batch].cpu().numpy().tobytes()
-        ok = ok and got == ref
+    B = args.batches or c["batches"]
+    wl = Workload(cfg, B, args.frames, torch, dev, libflac, synth, dec, seed=2 if cfg == "C2" else None)
+    elapsed, t_parse, t_decode = timed(wl, args.steps, args.warmup, stream, world, dist, dev)
+    ok = wl.check()
     if world > 1:
         o = torch.tensor([1 if ok else 0], device=dev)
         dist.all_reduce(o, op=dist.ReduceOp.MIN)
         ok = bool(o.item())
-
-    total_samples = samples_per_batch * B * args.steps * world
-    value = total_samples / elapsed / 1e6
-    alg_bytes = (fb_in + pcm_bytes_per_batch) * (B // G)   # per k_decode launch (one group)
-    achieved = alg_bytes / (t_decode * 1e-3) / 1e9
-    step_achieved = alg_bytes * G / (elapsed / args.steps) / 1e9
+    step_ms = elapsed / args.steps * 1e3
+    value = wl.samples * args.steps * world / elapsed / 1e6
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -334,36 +585,26 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": round(step_ms, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic: deterministic generator (seed 2), BASELINE C2 frame shape",
-        "config": {"workload": "C2: 1024-frame batches, 44.1 kHz/16-bit stereo, bs 4096, LPC-8, Rice partition "
-                               "order 4 -> FLACDecoder 16-bit LE interleaved PCM",
-                   "frames_per_batch": args.frames, "batches_per_step": B,
-                   "compressed_bytes_per_batch": fb_in, "pcm_bytes_per_batch": pcm_bytes_per_batch,
-                   "parallelism": f"frames sharded per rank x{world}",
-                   "pipeline": (f"{G} groups of {B // G} batches: k_parse(g+1) || k_decode(g) on two streams"
-                                if G > 1 else "serial: k_parse then k_decode over all batches")},
+        "data": f"synthetic: deterministic generator, BASELINE {cfg} frame shape",
+        "config": {"workload": c["desc"], "frames_per_batch": wl.nf1, "batches_per_step": B,
+                   "compressed_bytes_per_batch": wl.fb_in, "pcm_bytes_per_batch": wl.pcm1,
+                   "parallelism": f"frames sharded per rank x{world}"},
+        "per_gpu_value": round(value / world, 2),
         "bitexact": ok,
-        "roofline": {"bound": "hbm", "kernel": "k_decode", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(t_decode, 4),
-                     "k_parse_avg_ms": round(t_parse, 4), "step_achieved_GBs": round(step_achieved, 1),
-                     "launch": f"k_decode over one group ({B // G} batches x {args.frames} frames)"},
+        "roofline": roofline(wl.alg_bytes, t_decode, t_parse, step_ms, measured_traffic(cfg, B, wl.nf1)),
+        "kernels_sha": kernels_sha(),
     }
-    tr = measured_traffic(B, args.frames, G)
-    if tr is not None:
-        line["roofline"]["traffic"] = tr["traffic_bytes"]
-        line["roofline"]["traffic_source"] = tr["source"]
     if args.stats and rank == 0:
         import ctypes
         buf = (ctypes.c_uint64 * 16)()
         dec.L.bnflac_debug_stats(buf, 1)
         dec.L.bnflac_debug_set_ablate(0x100)
-        step()
+        wl.run(1, stream)
         torch.cuda.synchronize(dev)
         dec.L.bnflac_debug_stats(buf, 1)
         dec.L.bnflac_debug_set_ablate(0)
@@ -376,33 +617,28 @@ def main():
         abl = []
         for m in [int(x, 0) for x in args.ablate.split(",")]:
             dec.L.bnflac_debug_set_ablate(m)
-            run(1)
+            wl.run(1, stream)
             pe, de = [], []
-            run(args.steps, pe, de)
+            wl.run(args.steps, stream, pe, de)
             torch.cuda.synchronize(dev)
             abl.append({"ablate": m, "k_parse_ms": round(sum(a.elapsed_time(b) for a, b in pe) / len(pe), 4),
                         "k_decode_ms": round(sum(a.elapsed_time(b) for a, b in de) / len(de), 4)})
         dec.L.bnflac_debug_set_ablate(0)
         line["ablation"] = abl
     if rank == 0 and not args.no_index:
-        line["indexer"] = index_leg(torch, dev, libflac, dec, data, offs, sp)
+        line["indexer"] = index_leg(wl)
     if rank == 0 and not args.no_reader:
-        line["reader"] = reader_leg(libflac, data, s.pcm.astype("<i2").tobytes(), samples_per_batch)
+        line["reader"] = reader_leg(wl)
     if rank == 0 and not args.no_pcie:
-        line["pcie_inclusive"] = pcie_inclusive(args, torch, dev, libflac, dec, data, offs, sp, p, s,
-                                                pcm_bytes_per_batch, samples_per_batch)
+        line["pcie_inclusive"] = pcie_inclusive(wl)
     if rank == 0 and not args.no_cpu_baseline:
         sys.stdout.flush()
-        nthr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        mss1, passes1, el1 = cpu_baseline(data, samples_per_batch, args.cpu_seconds / 2, 1)
-        mss, passes, el = cpu_baseline(data, samples_per_batch, args.cpu_seconds / 2, nthr)
-        line["cpu_baseline"] = {"value": round(mss, 3), "unit": "MSamples/s", "cores": nthr, "kind": "port",
-                                "sample": f"{passes} x one C2 batch ({args.frames} frames, {samples_per_batch} samples) "
-                                          f"through the oracle's FLACDecoder.CopyTo replay on {nthr} threads, "
-                                          f"{el:.1f} s",
-                                "single_thread": {"value": round(mss1, 3), "cores": 1, "passes": passes1,
-                                                  "seconds": round(el1, 2)},
-                                "cpu": cpu_model()}
+        line["cpu_baseline"] = cpu_leg(wl, args.cpu_seconds, args.cpu_threads)
+    legs = [x for x in args.legs.split(",") if x and x != cfg] if world == 1 else []
+    if legs:
+        del wl
+        torch.cuda.empty_cache()
+        line["legs"] = {x: leg(x, args, torch, dev, libflac, synth, dec, stream) for x in legs}
     if rank == 0:
         js = json.dumps(line)
         print(js, flush=True)

@@ -37,8 +37,15 @@ typedef struct {
     uint32_t crc_ok;
     uint32_t sub_start[8];  /* bit offset of each subframe header, relative to frame_off*8 */
     uint32_t flags;         /* BNF_FL_* */
-    uint32_t pad_;
+    uint32_t crc_next;      /* BNF_CN_*: CRC-16 of [frame_off, next frame's offset), from the coalesced
+                               CRC pass fused into k_parse's launch; 0 when not computed */
 } bnf_frame_info;
+
+/* crc_next: a frame whose footer ends exactly at frame_off + (crc_next & BNF_CN_LEN) passed
+ * its CRC-16 check iff BNF_CN_ZERO is set (the CRC of a whole frame, footer included, is 0) */
+#define BNF_CN_VALID 0x80000000u
+#define BNF_CN_ZERO 0x40000000u
+#define BNF_CN_LEN 0x3FFFFFFFu
 
 enum {
     BNF_FL_NEEDS_SLOW = 1u,

@@ -719,13 +719,12 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 #define PARSE_RD 8 /* ring slots per lane (8 KB of LDS per wave, 5 waves per SIMD); 4 slots: 8 waves but 3% slower */
 #endif
 /* One lane per candidate frame: header + cursor walk over subframes 0..C-2.  Also
- * flags frames with an LPC order above 8 (they go to k_decode<32>). */
-__global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint64_t nbytes,
-                                              const uint64_t *__restrict__ frame_offs, uint32_t nframes,
-                                              bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
-                                              uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate) {
-    __shared__ uint32_t ring[PARSE_RD * RING_LANE_DW];
-    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+ * flags frames with an LPC order above 8 (they go to k_decode<32>).  keep_cn: the CRC pass
+ * of the same launch owns the record's crc_next word (not written here). */
+DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const uint64_t *__restrict__ frame_offs,
+                     uint32_t nframes, const bnf_stream_params &sp, const uint64_t *__restrict__ out_sample_in,
+                     uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate, lds_u32 *ring,
+                     uint32_t f, bool keep_cn) {
     if (f >= nframes) return;
     bnf_frame_info fi;
     fi.status = BNF_ST_OK;
@@ -740,7 +739,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     fi.out_sample = 0;
     fi.crc8 = fi.crc16_calc = fi.crc16_read = fi.crc_ok = 0;
     fi.flags = 0;
-    fi.pad_ = 0;
+    fi.crc_next = 0;
     /* sub_start is kept in registers and written by select chains: indexing fi.sub_start
      * with the runtime channel would put the whole record in scratch */
     uint32_t ss[8];
@@ -749,7 +748,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     const uint64_t limit = nbytes * 8u;
     const uint64_t fbit = fi.frame_off * 8u;
     BR b;
-    br_init(b, words, nbytes, (lds_u32 *)ring, threadIdx.x, PARSE_RD);
+    br_init(b, words, nbytes, ring, threadIdx.x, PARSE_RD);
     uint32_t st = parse_header(b, fbit, limit, sp, fi);
     if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
     if (st == BNF_ST_OK) {
@@ -800,7 +799,14 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     fi.status = st;
 #pragma unroll
     for (int c = 0; c < 8; c++) fi.sub_start[c] = ss[c];
-    info[f] = fi;
+    if (keep_cn) { /* every word but crc_next (written concurrently by the CRC pass) */
+        const uint32_t *src = (const uint32_t *)&fi;
+        uint32_t *dst = (uint32_t *)&info[f];
+#pragma unroll
+        for (int i = 0; i < 31; i++) dst[i] = src[i];
+    } else {
+        info[f] = fi;
+    }
 }
 
 #endif /* BNF_TU == 0 */
@@ -1083,6 +1089,109 @@ DEV uint32_t crc16_shift(uint32_t crc, uint64_t nbytes) {
     return crc;
 }
 
+#if BNF_TU == 0
+/* ============================================================== k_parse launch
+ * One launch, two kinds of single-wave workgroups, interleaved by block index:
+ *  - parse blocks: parse_frame, one lane per frame (lane-serial subframe walk);
+ *  - CRC blocks: one wave per frame, CRC_FPW consecutive frames each: the CRC-16 of
+ *    [offset f, offset f+1) (read_frame_'s footer check @0x10011a01 for a frame that ends
+ *    where the next one starts) over coalesced 1 KB wave loads.
+ * The walk is latency-bound and the CRC pass streams, so they share the chip; the decode
+ * kernels then skip their own lane-scattered CRC re-read (crc_next, BNF_CN_*).
+ * CRC layout: 16-byte pieces counted back from e = round_up(b1, 16); lane l takes pieces
+ * 63 - l + 64 m, so every wave load is 64 consecutive pieces.  Each lane runs a CRC over
+ * its own pieces with the 1008 bytes between them as zeros (x^(8*1008) by table), shifts
+ * the result to e (x^(8*16*(63 - l))), and the lanes are XOR-reduced: the CRC of the range
+ * times x^(8(e - b1)), which is 0 iff the range's CRC is 0 (x is invertible mod P).  Bytes
+ * outside [b0, b1) are masked to 0 (leading zeros leave a zero-initialised CRC at 0). */
+#define CRC_FPW 16
+
+DEV uint32_t crc_mulk(uint32_t a, const lds_u16 *TK) { return TK[a & 0xffu] ^ TK[256u + (a >> 8)]; }
+DEV uint32_t byte_keep(int32_t lo, int32_t hi, int32_t w) { /* bytes 4w..4w+3 kept iff in [lo, hi) */
+    const int32_t a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
+    const uint32_t mlo = a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
+    const uint32_t mhi = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    return mlo & mhi;
+}
+
+DEV void crc_frames(const uint8_t *__restrict__ bytes, uint64_t nbytes, const uint64_t *__restrict__ offs,
+                    uint32_t nframes, uint32_t f0, bnf_frame_info *__restrict__ info, const lds_u16 *T,
+                    const lds_u16 *TK, uint32_t lanec, uint32_t lane) {
+    const uint32_t fe = min(f0 + CRC_FPW, nframes);
+    for (uint32_t f = f0; f < fe; f++) {
+        const uint64_t b0 = offs[f];
+        const uint64_t b1 = f + 1u < nframes ? offs[f + 1u] : 0ull;
+        uint32_t word = 0;
+        if (b1 > b0 && b1 <= nbytes && b1 - b0 <= BNF_CN_LEN) { /* wave-uniform */
+            const uint64_t e = (b1 + 15u) & ~15ull, a0 = b0 & ~15ull;
+            const uint32_t np = (uint32_t)((e - a0) >> 4), M = (np + 63u) >> 6;
+            uint32_t acc = 0;
+            for (uint32_t m0 = 0; m0 < M; m0 += 4u) {
+                uint4 v[4];
+                uint64_t pp[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t m = m0 + (uint32_t)u;
+                    const uint32_t r = 63u - lane + 64u * (M - 1u - min(m, M - 1u));
+                    pp[u] = e - 16ull * (r + 1u);
+                    v[u] = (m < M && r < np) ? *(const uint4 *)(bytes + pp[u]) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (m0 + (uint32_t)u >= M) break; /* wave-uniform */
+                    const int64_t lo = (int64_t)b0 - (int64_t)pp[u], hi = (int64_t)b1 - (int64_t)pp[u];
+                    const bool edge = lo > 0 || hi < 16;
+                    if (any_lane(edge)) {
+                        if (edge) {
+                            const int32_t l32 = (int32_t)max(min(lo, (int64_t)16), (int64_t)0);
+                            const int32_t h32 = (int32_t)max(min(hi, (int64_t)16), (int64_t)0);
+                            v[u].x &= byte_keep(l32, h32, 0);
+                            v[u].y &= byte_keep(l32, h32, 1);
+                            v[u].z &= byte_keep(l32, h32, 2);
+                            v[u].w &= byte_keep(l32, h32, 3);
+                        }
+                    }
+                    acc = crc_mulk(acc, TK);
+                    acc = crc16_step8(acc, __builtin_bswap32(v[u].x), __builtin_bswap32(v[u].y), T);
+                    acc = crc16_step8(acc, __builtin_bswap32(v[u].z), __builtin_bswap32(v[u].w), T);
+                }
+            }
+            acc = gf_mul(acc, lanec);
+            for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
+            word = BNF_CN_VALID | (acc == 0u ? BNF_CN_ZERO : 0u) | (uint32_t)(b1 - b0);
+        }
+        if (lane == 0) info[f].crc_next = word;
+    }
+}
+
+__global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint64_t nbytes,
+                                              const uint64_t *__restrict__ frame_offs, uint32_t nframes,
+                                              bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
+                                              uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate,
+                                              uint32_t nparse, uint32_t ncrc) {
+    __shared__ uint32_t ring[PARSE_RD * RING_LANE_DW]; /* parse: the bit ring; CRC: the tables */
+    static_assert(PARSE_RD * RING_LANE_DW * 4 >= (8 * 256 + 512) * 2, "CRC tables fit the ring");
+    const uint32_t lane = threadIdx.x;
+    const uint32_t tot = nparse + ncrc, b = blockIdx.x;
+    const uint32_t pb = (uint32_t)((uint64_t)b * nparse / tot), pb1 = (uint32_t)((uint64_t)(b + 1u) * nparse / tot);
+    if (pb1 > pb) {
+        parse_frame(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
+                    pb * 64u + lane, ncrc != 0);
+        return;
+    }
+    lds_u16 *T = (lds_u16 *)(lds_u32 *)ring, *TK = T + 8 * 256;
+    for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
+    const uint32_t K = crc16_shift(1u, 1008u); /* x^(8*1008) mod P */
+    for (uint32_t i = lane; i < 256u; i += 64u) {
+        TK[i] = (uint16_t)gf_mul(i, K);
+        TK[256u + i] = (uint16_t)gf_mul(i << 8, K);
+    }
+    const uint32_t lanec = crc16_shift(1u, 16u * (63u - lane));
+    __syncthreads();
+    crc_frames((const uint8_t *)words, nbytes, frame_offs, nframes, (b - pb) * CRC_FPW, info, T, TK, lanec, lane);
+}
+#endif
+
 /* Channel decorrelation (read_frame_ @0x10011a37-0x10011adb), 32-bit wrap. */
 DEV void decorrelate(uint32_t as, int32_t &v0, int32_t &v1) {
     if (as == 1) v1 = (int32_t)((uint32_t)v0 - (uint32_t)v1);
@@ -1200,13 +1309,13 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
     static_assert(MAXW <= CHK && CHK % 8 == 0 && RD <= RING_MAX, "chunk must hold the predictor ring");
     __shared__ uint32_t ring[RD * RING_LANE_DW];
     __shared__ int32_t lds[CHK * RP]; /* [sample][lane] */
-    static_assert(CHK * RP >= 1024 + 448, "row buffer also holds the CRC tables and the tail's frame table");
+    static_assert(CHK * RP >= 1024 + 512, "row buffer also holds the CRC tables and the tail's frame table");
     /* per-frame tables overlay the buffers while those are idle: the setup exchange uses
      * the ring before its first DMA, the tail uses the row buffer after the last pack */
     uint32_t *f_bs = ring, *f_ch = ring + 64, *f_as = ring + 128, *f_ok = ring + 192;
     uint64_t *f_out = (uint64_t *)(ring + 256);
     uint32_t *t_bs = (uint32_t *)lds + 1024, *t_ch = t_bs + 64, *t_ok = t_bs + 128, *t_endbit = t_bs + 192,
-             *t_bad = t_bs + 256;
+             *t_bad = t_bs + 256, *t_pre = t_bs + 448;
     uint64_t *t_out = (uint64_t *)(t_bs + 320);
 
     const uint32_t lane = threadIdx.x;
@@ -1449,7 +1558,7 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
 
     /* ---- last subframe end, zero padding, CRC-16 (read_frame_ @0x100118c0 tail).  The
      * frame record is re-read here (only scalars stay live across the chunk loop). */
-    if (lane < fpb) { t_ok[lane] = 0; t_bad[lane] = 0; t_endbit[lane] = 0; }
+    if (lane < fpb) { t_ok[lane] = 0; t_bad[lane] = 0; t_endbit[lane] = 0; t_pre[lane] = 0; }
     lds_sync();
     if (have && ch == 0) {
         t_ok[fl] = fok ? 1u : 0u;
@@ -1497,19 +1606,27 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
                     t_crc_read = crc_read;
                     t_resume = br_pos(b);
                     t_resume_set = true;
+                    /* the k_parse launch's CRC pass found this frame's CRC-16 zero */
+                    const uint32_t cn = info[f].crc_next;
+                    if ((cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && f_off + (cn & BNF_CN_LEN) == end_byte + 2u)
+                        t_pre[fl] = 1u;
                 }
             }
         }
         if (t_status != BNF_ST_OK) t_bad[fl] = 1;
     }
-    /* the rows are free now: stage the slice-by-8 CRC tables there */
-    lds_u16 *T = (lds_u16 *)(lds_u32 *)lds;
-    for (uint32_t i = lane; i < 8u * 256u; i += DEC_LANES) T[i] = (&g_crc16_tab[0][0])[i];
-    __syncthreads();
-    /* CRC-16 over [frame_off, end): split across the frame's channel lanes, combined by
-     * polynomial shifts (CRC is linear: crc(A|B) = crc(A)*x^(8|B|) + crc(B)). */
+    lds_sync();
+    /* CRC-16 over [frame_off, end) for frames the CRC pass did not vouch for: split across
+     * the frame's channel lanes, combined by polynomial shifts (CRC is linear:
+     * crc(A|B) = crc(A)*x^(8|B|) + crc(B)). */
     uint32_t part = 0;
-    const bool crc_lane = fok && frame_ok && ch < fch && !t_bad[fl];
+    const bool crc_lane = fok && frame_ok && ch < fch && !t_bad[fl] && !t_pre[fl];
+    lds_u16 *T = (lds_u16 *)(lds_u32 *)lds;
+    if (__any(crc_lane)) { /* the rows are free now: stage the slice-by-8 CRC tables there */
+        __syncthreads();
+        for (uint32_t i = lane; i < 8u * 256u; i += DEC_LANES) T[i] = (&g_crc16_tab[0][0])[i];
+        __syncthreads();
+    }
     if (crc_lane) {
         const uint64_t len = t_endbit[fl];
         const uint32_t nl = fch;
@@ -1523,7 +1640,7 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
     /* xor-reduce within each frame's lane group */
     uint32_t acc = part;
     for (uint32_t o = 1; o < chn_lanes; o <<= 1) acc ^= __shfl_xor(acc, o);
-    if ((ablate & 1u) && last && t_status == BNF_ST_OK) acc = t_crc_read;
+    if (((ablate & 1u) || t_pre[fl]) && last && t_status == BNF_ST_OK) acc = t_crc_read;
     if (last) {
         bnf_frame_info fo = info[f];
         fo.status = t_status;
@@ -2384,13 +2501,23 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         if (br_pos(z1.b) > limit) ok = false;
         resume = br_pos(z1.b);
     }
-    wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
-    lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
-    for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
-    __syncthreads();
-    uint32_t crc = 0;
-    if (ok && !(ablate & 1u)) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
-    if ((ablate & 1u) && ok) crc = crc_read;
+    /* CRC-16: the k_parse launch's coalesced CRC pass covered [frame_off, next offset); a
+     * frame whose footer ends there and whose CRC was 0 is done.  Otherwise (the last frame
+     * of a batch, a gap before the next offset, a mismatch) the frame is re-read here. */
+    uint32_t crc = crc_read;
+    bool need = false;
+    if (ok) {
+        const uint32_t cn = info[f].crc_next;
+        const bool pre = (cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && fi.frame_off + (cn & BNF_CN_LEN) == end_byte + 2u;
+        need = !pre && !(ablate & 1u);
+    }
+    if (any_lane(need)) {
+        wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
+        lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
+        for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
+        __syncthreads();
+        if (need) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
+    }
     if (ok && crc != crc_read) ok = false;
     if (ok) {
         info[f].resume_bit = resume;
@@ -2575,12 +2702,14 @@ hipError_t bnf_stats(uint64_t *out16, int reset) {
 }
 
 /* words: 16-byte aligned; the allocation must cover round_up(nbytes, 16) bytes. */
+/* crc: also run the coalesced CRC pass over [offset f, offset f+1) (info.crc_next) */
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
                             bnf_stream_params sp, const uint64_t *out_sample_in, uint64_t base_sample,
-                            bnf_frame_info *info, hipStream_t s) {
+                            bnf_frame_info *info, int crc, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
-    hipLaunchKernelGGL(k_parse, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
-                       out_sample_in, base_sample, info, ablate_flags());
+    const uint32_t np = (nframes + 63) / 64, nc = crc ? (nframes + CRC_FPW - 1) / CRC_FPW : 0u;
+    hipLaunchKernelGGL(k_parse, dim3(np + nc), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
+                       out_sample_in, base_sample, info, ablate_flags(), np, nc);
     return hipGetLastError();
 }
 

@@ -44,7 +44,7 @@ void bnf_set_ablate(uint32_t v);
 hipError_t bnf_stats(uint64_t *out16, int reset);
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs,
                             uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
-                            uint64_t base_sample, bnf_frame_info *info, hipStream_t s);
+                            uint64_t base_sample, bnf_frame_info *info, int crc, hipStream_t s);
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes,
                              bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
                              bnf_frame_info *info, hipStream_t s);
@@ -117,6 +117,19 @@ static int ensure_device(int dev) {
  * wrong while non-zero.  bit0 CRC-16, bit1 PCM stores, bit2 restore, bit3 Rice decode,
  * bit4 k_parse subframe walk. */
 extern "C" BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags) { bnf_set_ablate(flags); }
+/* Coalesced CRC pass fused into the k_parse launch of the batch API (frame record
+ * crc_next; the decode kernels then skip their own CRC re-read for frames it vouches for).
+ * Off by default: on C2 it costs the parse launch more (+2.4 ms at B = 1024) than it saves
+ * the decode launch (-1.2 ms), see DESIGN.md section 9.  BNFLAC_CRC_PASS=1 turns it on. */
+static int g_crc_pass = -1;
+static int crc_pass() {
+    if (g_crc_pass < 0) {
+        const char *e = getenv("BNFLAC_CRC_PASS");
+        g_crc_pass = (e && atoi(e) != 0) ? 1 : 0;
+    }
+    return g_crc_pass;
+}
+extern "C" BNFLAC_API void bnflac_debug_set_crc_pass(int on) { g_crc_pass = on ? 1 : 0; }
 extern "C" BNFLAC_API int bnflac_debug_stats(uint64_t *out16, int reset) {
     return bnf_stats(out16, reset) == hipSuccess ? 0 : fail("bnflac_debug_stats failed");
 }
@@ -234,7 +247,8 @@ extern "C" BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, d_frame_offsets,
-                                    nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info, (hipStream_t)hs);
+                                    nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info, crc_pass(),
+                                    (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_parse: ") + hipGetErrorString(e));
 }
 
@@ -294,7 +308,7 @@ extern "C" BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_
     memcpy(&p, sp, sizeof p);
     /* 2. header, CRC-8 and subframe walk of every candidate */
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, p, nullptr,
-                                    0, (bnf_frame_info *)ctx->info.p, s);
+                                    0, (bnf_frame_info *)ctx->info.p, 0, s);
     /* 3. successor chain, EOS rule, compaction */
     if (e == hipSuccess)
         e = bnf_launch_chain(d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, (const bnf_frame_info *)ctx->info.p,
@@ -701,7 +715,7 @@ bool decode_window(Dec *d, uint64_t base) {
             const uint32_t pcm_ch = 8; /* planar slots sized for any channel count */
             if (!d->d_info.grow(sizeof(bnf_frame_info) * ncand)) goto oom;
             if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, n, (const uint64_t *)d->d_cand.p, ncand, sp,
-                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, d->stream) != hipSuccess)
+                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, 0, d->stream) != hipSuccess)
                 goto hip_fail;
             if (hipMemcpyAsync(d->info.data(), d->d_info.p, sizeof(bnf_frame_info) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
                 goto hip_fail;

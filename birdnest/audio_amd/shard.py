@@ -38,6 +38,10 @@ def partition(samples_per_frame: Sequence[int], world: int) -> List[Tuple[int, i
 def gather_bytes(local, group=None, dst: int = 0):
     """Gather variable-length uint8 tensors to rank `dst` (concatenated in rank order).
 
+    Sizes go first (all_gather of one int64); then `dst` posts every receive at once and
+    the other ranks send, as one batch of point-to-point ops (dist.batch_isend_irecv: a
+    grouped ncclSend/ncclRecv under RCCL), so the peers' transfers run concurrently over
+    their own xGMI links instead of one link at a time.  RCCL has no gatherv.
     Returns the concatenation on `dst`, None elsewhere.  Works with the gloo (CPU tensors)
     and nccl/RCCL (device tensors) backends.
     """
@@ -50,17 +54,16 @@ def gather_bytes(local, group=None, dst: int = 0):
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     sizes = [int(s.item()) for s in sizes]
+    glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
     if rank == dst:
-        parts = []
-        for r in range(world):
-            if r == rank:
-                parts.append(local)
-            else:
-                buf = torch.empty(sizes[r], dtype=local.dtype, device=local.device)
-                if sizes[r]:
-                    dist.recv(buf, src=r, group=group)
-                parts.append(buf)
+        parts = [local if r == rank else torch.empty(sizes[r], dtype=local.dtype, device=local.device)
+                 for r in range(world)]
+        ops = [dist.P2POp(dist.irecv, parts[r], glob(r), group) for r in range(world) if r != rank and sizes[r]]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
         return torch.cat(parts)
     if local.numel():
-        dist.send(local, dst=dst, group=group)
+        for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), glob(dst), group)]):
+            req.wait()
     return None

@@ -106,7 +106,9 @@ typedef struct {
     uint64_t out_sample;
     uint32_t crc8, crc16_calc, crc16_read, crc_ok;
     uint32_t sub_start[8];
-    uint32_t flags, pad_;
+    uint32_t flags;
+    uint32_t crc_next;      /* k_parse's CRC pass: bit31 valid, bit30 CRC-16 of [frame_off, next offset) is 0,
+                               bits 0-29 that length (0 when not computed) */
 } bnflac_frame_info;
 
 enum {
@@ -174,6 +176,10 @@ BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uin
 /* Timing experiments only: skip parts of the kernels (bit0 CRC-16, bit1 PCM stores,
  * bit2 restore, bit3 Rice decode, bit4 subframe walk).  Output is wrong while set. */
 BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags);
+/* Mode switch (results stay exact): run the coalesced CRC-16 pass in bnflac_parse_frames'
+ * launch (frame record crc_next) so the decode kernels skip their own CRC re-read for the
+ * frames it vouches for.  Default off (env BNFLAC_CRC_PASS=1 turns it on). */
+BNFLAC_API void bnflac_debug_set_crc_pass(int on);
 /* Debug: k_decode event counters collected while ablate bit 0x100 is set: [0..5] fused
  * chunks, generic chunks, DMA landing waits, slow Rice codewords, refills, waves (wave-level
  * events); [8..12] shader-clock cycles summed over waves in setup, chunk decode, refill,

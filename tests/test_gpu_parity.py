@@ -215,6 +215,45 @@ def test_crc_mismatch_zero_filled_in_batch(gpu):
                           np.delete(s.pcm, np.s_[2 * 4096: 3 * 4096], axis=0))
 
 
+def test_crc_pass_records_and_fallbacks(gpu):
+    """The coalesced CRC pass of the k_parse launch (frame record crc_next): valid and zero for
+    intact frames followed by another offset, not zero for a corrupted frame, absent for the
+    last frame; frames whose footer does not end at the next offset (junk in between) and the
+    last frame still get their CRC-16 checked by the decode kernels themselves."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    libflac.load().bnflac_debug_set_crc_pass(1)
+    try:
+        _crc_pass_cases(gpu, synth, libflac)
+    finally:
+        libflac.load().bnflac_debug_set_crc_pass(0)
+
+
+def _crc_pass_cases(gpu, synth, libflac):
+    for cfg in ("C2", "C3", "C4"):
+        s = synth.encode(synth.config(cfg, nframes=8, last_blocksize=0))
+        d = bytearray(s.data.tobytes())
+        o = [int(x) for x in s.frame_offsets]
+        d[o[2] + 100] ^= 0x40                       # frame 2: CRC mismatch
+        junk = bytes([0x5A, 0x00, 0x13] * 7)         # 21 bytes of junk between frames 5 and 6
+        d = d[: o[6]] + junk + d[o[6]:]
+        o = o[:6] + [x + len(junk) for x in o[6:]]
+        out, info, sp = _decode_batch(gpu, bytes(d), o, libflac.OUT_INTERLEAVED32)
+        cn = info["crc_next"].astype(np.int64)
+        valid, zero, ln = (cn >> 31) & 1, (cn >> 30) & 1, cn & 0x3FFFFFFF
+        assert valid[:7].all() and valid[7] == 0, cfg
+        assert list(ln[:7]) == [o[i + 1] - o[i] for i in range(7)], cfg
+        assert zero[2] == 0 and zero[5] == 0 and zero[[0, 1, 3, 4, 6]].all(), cfg
+        assert info["crc_ok"].tolist() == [1, 1, 0, 1, 1, 1, 1, 1], cfg
+        assert (info["status"] == 0).all(), cfg
+        pcm = out.view("<i4").reshape(-1, s.pcm.shape[1])
+        bs = s.params.blocksize if not s.params.variable_blocksize else None
+        if bs:
+            assert not pcm[2 * bs: 3 * bs].any(), cfg
+            assert np.array_equal(np.delete(pcm, np.s_[2 * bs: 3 * bs], axis=0),
+                                  np.delete(s.pcm, np.s_[2 * bs: 3 * bs], axis=0)), cfg
+
+
 # ---------------------------------------------------------- libFLAC API parity
 STREAM_CASES = [k for k, v in GOLD.items() if v["kind"] in ("roundtrip", "error", "rfc")]
 

@@ -82,3 +82,38 @@ def test_two_rank_gather_matches_whole_stream():
         pr.join(timeout=60)
         assert pr.exitcode == 0
     assert got == s.pcm.astype("<i2").tobytes()
+
+
+def _gather_worker(rank, world, port, sizes, result_q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        local = torch.full((sizes[rank],), rank + 1, dtype=torch.uint8)
+        got = shard.gather_bytes(local)
+        if rank == 0:
+            result_q.put(got.numpy().tobytes())
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_concurrent_gather_three_ranks_ragged():
+    """shard.gather_bytes posts every receive at once (batch_isend_irecv): ragged sizes,
+    one rank with nothing to send, concatenated in rank order on rank 0."""
+    import torch.multiprocessing as mp
+    sizes = [5, 0, 70001]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 3, port, sizes, q)) for r in range(3)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=120)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert got == bytes([1] * 5 + [3] * 70001)
