@@ -51,9 +51,10 @@ enum {
     BNF_FL_NEEDS_SLOW = 1u,
     BNF_FL_OUT_OF_BOUNDS = 2u, /* set by k_decode: frame would end past out_bytes (SKIPPED) */
     BNF_FL_UNSUPPORTED = 4u,   /* set by k_decode: the output format cannot carry the frame (SKIPPED) */
-    BNF_FL_W32 = 16u,          /* set by k_parse: an LPC order > 8 (decoded by k_decode<32>) */
+    BNF_FL_W32 = 16u,          /* set by k_parse: an LPC order > 16 (decoded by k_decode<32>) */
     BNF_FL_ST = 32u,           /* set by k_parse: 2-channel frame, LPC orders <= 8 (k_decode_st's candidates) */
-    BNF_FL_REDO = 64u          /* set by k_decode_st: declined (rare case), decoded again by k_decode<8> */
+    BNF_FL_REDO = 64u,         /* set by k_decode_st: declined (rare case), decoded again by k_decode<8> */
+    BNF_FL_W16 = 128u          /* set by k_parse: LPC orders 9..16, or LPC above 16 bits (k_decode<16>) */
 };
 
 /* Output formats of k_decode */

@@ -793,8 +793,12 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
                 break;
             }
         }
-        if (maxorder > 8) fi.flags |= BNF_FL_W32;
-        else if (fi.channels == 2) fi.flags |= BNF_FL_ST;
+        /* decode instance: LPC orders above 16 -> k_decode<32>; 9..16, or LPC at more than 16
+         * bits (libFLAC's 64-bit restore is then the usual path) -> k_decode<16>; 16-bit stereo
+         * otherwise -> k_decode_st; the rest -> k_decode<8> */
+        if (maxorder > 16) fi.flags |= BNF_FL_W32;
+        else if (maxorder > 8 || (maxorder > 0 && fi.bps > 16)) fi.flags |= BNF_FL_W16;
+        else if (fi.channels == 2 && fi.bps <= 16) fi.flags |= BNF_FL_ST;
     }
     fi.status = st;
 #pragma unroll
@@ -921,10 +925,13 @@ DEV int32_t lpc_pred(const int32_t (&c)[N], const int32_t (&h)[N], const int32_t
         const int32_t sum = (int32_t)(((uint32_t)shi << 12) + (uint32_t)slo);
         return sum >> sh;
     } else {
-        int64_t sum = 0;
+        /* exact 64-bit products (v_mad_i64_i32, as fast as v_mad_i32_i24 on gfx950:
+         * tools/ubench_mad.hip) in two independent chains: the dependent-MAC latency
+         * (~12 cycles), not the issue rate, bounds a lane-per-subframe kernel */
+        int64_t s2[2] = {0, 0};
 #pragma unroll
-        for (int t = 0; t < W; t++) sum += (int64_t)c[t] * (int64_t)h[((i - 1 - t) % W + W) % W];
-        return (int32_t)(sum >> sh);
+        for (int t = 0; t < W; t++) s2[t & 1] += (int64_t)c[t] * (int64_t)h[((i - 1 - t) % W + W) % W];
+        return (int32_t)((s2[0] + s2[1]) >> sh);
     }
 }
 
@@ -965,6 +972,22 @@ DEV void lpc_chunk(int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t
 /* Fused Rice decode + LPC restore of a full chunk past the warm-up, inside one Rice
  * partition (parameter k, not escaped): the residual never leaves registers and the
  * two dependency chains (bit cursor, predictor) interleave. */
+/* samples T..W-1 of one W-sample group, unrolled by recursion so every history index is a
+ * compile-time constant (a rolled loop puts the ring behind s_set_gpr_idx moves) */
+template <int T, int W, int P, int N>
+DEV void lpc_fused_steps(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
+                         int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc, PendW &pw, int j) {
+    if constexpr (T < W) {
+        const int32_t r = rice_one(b, k, limit, trunc, &pw);
+        const int32_t s = (int32_t)((uint32_t)r + (uint32_t)lpc_pred<W, P>(c, h, ht, T, sh));
+        lpc_push<W, P>(h, ht, T, s);
+        pw.v = (int32_t)((uint32_t)s << wasted);
+        pw.at = row + (j + T) * RP;
+        pw.on = true;
+        lpc_fused_steps<T + 1, W, P, N>(b, k, row, c, h, ht, sh, wasted, limit, trunc, pw, j);
+    }
+}
+
 template <int CH, int W, int P, int N>
 DEV void lpc_fused(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
                    int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc) {
@@ -975,17 +998,7 @@ DEV void lpc_fused(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32
     pw.v = 0;
     pw.on = false;
 #pragma unroll 1
-    for (int j = 0; j < CH; j += W) {
-#pragma unroll
-        for (int t = 0; t < W; t++) {
-            const int32_t r = rice_one(b, k, limit, trunc, &pw);
-            const int32_t s = (int32_t)((uint32_t)r + (uint32_t)lpc_pred<W, P>(c, h, ht, t, sh));
-            lpc_push<W, P>(h, ht, t, s);
-            pw.v = (int32_t)((uint32_t)s << wasted);
-            pw.at = row + (j + t) * RP;
-            pw.on = true;
-        }
-    }
+    for (int j = 0; j < CH; j += W) lpc_fused_steps<0, W, P, N>(b, k, row, c, h, ht, sh, wasted, limit, trunc, pw, j);
     *pw.at = pw.v;
 }
 
@@ -1206,21 +1219,36 @@ DEV void decorrelate(uint32_t as, int32_t &v0, int32_t &v1) {
 
 /* Pack one chunk: every lane writes a contiguous run of CH/chn_lanes samples of its own
  * frame (metadata in registers), reading the frame's channel rows from LDS.  Stereo
- * FLACDecoder / interleaved-int32 runs go out as 16-byte stores. */
-/* returns the path taken: 0 nothing stored, 1 vector fast path (pack_fast_stores<FMT,CH>
- * store instructions), 2 generic per-sample path */
+ * FLACDecoder / interleaved-int32 runs go out as 16-byte stores; FLACFileReader runs (2 or
+ * 3 bytes per value, all channels) are packed into dwords in registers and go out as 16-,
+ * 4- or 1-byte stores by alignment.  Returns how many store instructions this lane issued
+ * (the caller takes the wave minimum over storing lanes: a lower bound on the wave's
+ * stores keeps the refill's counted vmcnt wait exact or conservative). */
 template <int FMT, int CH> constexpr uint32_t pack_fast_stores() { return FMT == BNF_OUT_INTERLEAVED32 ? CH / 4 : CH / 8; }
+
+/* 4 values of fb bytes each (little-endian) -> fb dwords of the byte stream */
+DEV void pack4(const int32_t (&v)[4], uint32_t fb, uint32_t (&d)[3]) {
+    if (fb == 3) {
+        d[0] = ((uint32_t)v[0] & 0xFFFFFFu) | ((uint32_t)v[1] << 24);
+        d[1] = (((uint32_t)v[1] >> 8) & 0xFFFFu) | ((uint32_t)v[2] << 16);
+        d[2] = (((uint32_t)v[2] >> 16) & 0xFFu) | ((uint32_t)v[3] << 8);
+    } else {
+        d[0] = ((uint32_t)v[0] & 0xFFFFu) | ((uint32_t)v[1] << 16);
+        d[1] = ((uint32_t)v[2] & 0xFFFFu) | ((uint32_t)v[3] << 16);
+        d[2] = 0;
+    }
+}
+
 template <int FMT, int CH>
 DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, uint32_t n0, bool fok, uint32_t bs,
-                   uint32_t C, uint32_t as, uint64_t os, uint32_t stream_channels, uint32_t fr_bytes,
-                   uint8_t *__restrict__ out) {
+                       uint32_t C, uint32_t as, uint64_t os, uint32_t stream_channels, uint32_t fr_bytes,
+                       uint8_t *__restrict__ out) {
     const uint32_t per = CH / chn_lanes;
     const uint32_t fl = lane / chn_lanes, part = lane % chn_lanes;
     const uint32_t i0 = part * per;
     if (!fok || n0 + i0 >= bs) return 0;
     const uint32_t cnt = min(per, bs - (n0 + i0));
     const int32_t *rows = lds + i0 * RP + fl * chn_lanes; /* channel c of sample q: rows[q * RP + c] */
-    const uint64_t s0 = os + n0 + i0; /* first output sample of this run */
     const uint32_t bpsmp = (FMT == BNF_OUT_INTERLEAVED32) ? 8u : 4u;
     /* vector path (stereo): the frame's two lanes take interleaved 4-sample groups
      * (lane h: samples 8g+4h .. 8g+4h+3), so each 16-byte store instruction writes 32
@@ -1250,8 +1278,82 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
                 *(int4 *)(base + i * 8u + 16u) = make_int4(l[2], r[2], l[3], r[3]);
             }
         }
-        return 1;
+        return pack_fast_stores<FMT, CH>();
     }
+    if (FMT == BNF_OUT_FILEREADER && C == stream_channels) { /* FLACFileReader.cs:220-237 */
+        /* the run: cnt samples x C channels, values slot-ordered (sample-major), fb bytes each;
+         * per is a multiple of 4, so full runs are whole groups of 4 values = fb dwords */
+        const uint32_t fb = fr_bytes, slots = cnt * C;
+        uint8_t *o = out + (os + n0 + i0) * (uint64_t)stream_channels * fb;
+        const uintptr_t oa = (uintptr_t)o;
+        const uint32_t ngrp = slots >> 2, rem = slots & 3u;
+        const bool a16 = (oa & 15u) == 0 && (fb == 3 ? (ngrp & 3u) == 0 : (ngrp & 1u) == 0) && rem == 0;
+        const bool a4 = (oa & 3u) == 0 && rem == 0;
+        uint32_t nst = 0;
+        if (a16 || a4) {
+            /* the run's dwords in registers (compile-time indices: up to CH/4 groups of fb) */
+            uint32_t dw[CH / 4 * 3];
+#pragma unroll
+            for (int g = 0; g < CH / 4; g++) {
+                int32_t v[4] = {0, 0, 0, 0};
+                if ((uint32_t)g < ngrp) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t k = 4u * g + (uint32_t)u;
+                        const uint32_t q = k / C, c = k - q * C;
+                        v[u] = rows[q * RP + c];
+                    }
+                    if (C == 2) { /* stereo pairs are whole within a group of 4 */
+                        decorrelate(as, v[0], v[1]);
+                        decorrelate(as, v[2], v[3]);
+                    }
+                }
+                uint32_t d[3];
+                pack4(v, fb, d);
+                if (fb == 3) {
+                    dw[3 * g] = d[0];
+                    dw[3 * g + 1] = d[1];
+                    dw[3 * g + 2] = d[2];
+                } else { /* 16-bit: 2 dwords per group, packed densely */
+                    dw[2 * g] = d[0];
+                    dw[2 * g + 1] = d[1];
+                }
+            }
+            const uint32_t ndw = ngrp * fb;
+            if (a16) {
+#pragma unroll
+                for (int u = 0; u < CH * 3 / 16; u++)
+                    if ((uint32_t)(4 * u) < ndw) {
+                        *(uint4 *)(o + 16u * u) = make_uint4(dw[4 * u], dw[4 * u + 1], dw[4 * u + 2], dw[4 * u + 3]);
+                        nst++;
+                    }
+            } else {
+#pragma unroll
+                for (int u = 0; u < CH * 3 / 4; u++)
+                    if ((uint32_t)u < ndw) {
+                        *(uint32_t *)(o + 4u * u) = dw[u];
+                        nst++;
+                    }
+            }
+        } else { /* unaligned or ragged run: byte stores */
+            for (uint32_t k = 0; k < slots; k++) {
+                const uint32_t q = k / C, c = k - q * C;
+                int32_t v0 = rows[q * RP + c];
+                if (C == 2) { /* the pair of this sample */
+                    int32_t l = rows[q * RP], r = rows[q * RP + 1];
+                    decorrelate(as, l, r);
+                    v0 = c ? r : l;
+                }
+                uint8_t *p = o + (uint64_t)k * fb;
+                p[0] = (uint8_t)v0;
+                p[1] = (uint8_t)(v0 >> 8);
+                if (fb == 3) p[2] = (uint8_t)(v0 >> 16);
+                nst += fb;
+            }
+        }
+        return nst;
+    }
+    uint32_t nst = 0;
     for (uint32_t q = 0; q < cnt; q++) {
         const uint32_t n = n0 + i0 + q;
         int32_t v[8];
@@ -1261,9 +1363,11 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
         if (FMT == BNF_OUT_PLANAR32) {
             int32_t *o = (int32_t *)out + os * stream_channels;
             for (uint32_t c = 0; c < C; c++) o[(uint64_t)c * bs + n] = v[c];
+            nst += C;
         } else if (FMT == BNF_OUT_INTERLEAVED32) {
             int32_t *o = (int32_t *)out + (os + n) * stream_channels;
             for (uint32_t c = 0; c < C; c++) o[c] = v[c];
+            nst += C;
         } else if (FMT == BNF_OUT_FLACDECODER) { /* FLACDecoder.cs:543-577 */
             if (C == 2) {
                 uint32_t *o = (uint32_t *)out;
@@ -1272,6 +1376,7 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
                 uint16_t *o = (uint16_t *)out;
                 o[os + n] = (uint16_t)(uint32_t)v[0];
             }
+            nst += 1;
         } else { /* FLACFileReader.cs:220-237: 2 or 3 bytes per sample, all channels */
             uint8_t *o = out + (os + n) * (uint64_t)stream_channels * fr_bytes;
             for (uint32_t c = 0; c < C; c++) {
@@ -1279,30 +1384,23 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
                 o[c * fr_bytes + 1] = (uint8_t)(v[c] >> 8);
                 if (fr_bytes == 3) o[c * fr_bytes + 2] = (uint8_t)(v[c] >> 16);
             }
+            nst += C * fr_bytes;
         }
     }
-    return 2;
+    return nst;
 }
 
-#define LPC_DISPATCH(FN, W_, ...)                                                                   \
-    do {                                                                                             \
-        if (h.path == P_MMX16) {                                                                     \
-            if (W_ == 8) FN<CHK, 8, P_MMX16>(__VA_ARGS__);                                                \
-            else if (MAXW >= 16 && W_ == 16) FN<CHK, (MAXW >= 16 ? 16 : 8), P_MMX16>(__VA_ARGS__);        \
-            else if (MAXW >= 32) FN<CHK, (MAXW >= 32 ? 32 : 8), P_MMX16>(__VA_ARGS__);                    \
-        } else if (h.path == P_IA32) {                                                               \
-            if (W_ == 8) FN<CHK, 8, P_IA32>(__VA_ARGS__);                                                 \
-            else if (MAXW >= 16 && W_ == 16) FN<CHK, (MAXW >= 16 ? 16 : 8), P_IA32>(__VA_ARGS__);         \
-            else if (MAXW >= 32) FN<CHK, (MAXW >= 32 ? 32 : 8), P_IA32>(__VA_ARGS__);                     \
-        } else {                                                                                     \
-            if (W_ == 8) FN<CHK, 8, P_WIDE>(__VA_ARGS__);                                                 \
-            else if (MAXW >= 16 && W_ == 16) FN<CHK, (MAXW >= 16 ? 16 : 8), P_WIDE>(__VA_ARGS__);         \
-            else if (MAXW >= 32) FN<CHK, (MAXW >= 32 ? 32 : 8), P_WIDE>(__VA_ARGS__);                     \
-        }                                                                                            \
+/* restore-path dispatch (per lane); the tap count is the instance's (orders below it run
+ * with zero coefficients), so a wave takes at most one variant per libFLAC path */
+#define LPC_DISPATCH(FN, ...)                                                                     \
+    do {                                                                                           \
+        if (h.path == P_MMX16) FN<CHK, MAXW, P_MMX16>(__VA_ARGS__);                                \
+        else if (h.path == P_IA32) FN<CHK, MAXW, P_IA32>(__VA_ARGS__);                             \
+        else FN<CHK, MAXW, P_WIDE>(__VA_ARGS__);                                                   \
     } while (0)
 
 template <int MAXW, int CHK, int RD>
-__global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
+__global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : (MAXW == 16 ? 2 : 1)) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
                                                       uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                       int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
                                                       bnf_frame_info *__restrict__ info, uint32_t ablate) {
@@ -1330,8 +1428,13 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
     /* stereo frames are k_decode_st's, unless it handed them back (BNF_FL_REDO) */
     if (have && (fi.flags & BNF_FL_ST) && !(fi.flags & BNF_FL_REDO) && !(ablate & 0x400u)) have = false;
     const bool frame_ok = have && fi.status == BNF_ST_OK;
-    /* one wave per workgroup: the W=8 and W=32 instances split the blocks between them */
-    if ((MAXW == 32) != (__any(frame_ok && (fi.flags & BNF_FL_W32)) != 0)) return;
+    /* one wave per workgroup: the W = 8, 16 and 32 instances split the blocks between them
+     * by the widest class among the block's frames (k_parse's flags) */
+    {
+        const bool a32 = __any(frame_ok && (fi.flags & BNF_FL_W32)) != 0;
+        const bool a16 = __any(frame_ok && (fi.flags & BNF_FL_W16)) != 0;
+        if ((a32 ? 32 : (a16 ? 16 : 8)) != MAXW) return;
+    }
 
     bool active = frame_ok && ch < fi.channels && fi.channels <= chn_lanes;
     if (lane < fpb) { f_ok[lane] = 0; f_bs[lane] = 0; }
@@ -1461,7 +1564,6 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
     uint32_t mybs = active ? bs : 0u;
     for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
     const uint32_t nchunks = (mybs + CHK - 1) / CHK;
-    const uint32_t W = h.order <= 8 ? 8u : (h.order <= 16 ? 16u : 32u);
 
     const uint64_t t_loop = tnow(tmon);
     wait_vm(); /* setup loads done: the pipeline counts start from zero */
@@ -1483,7 +1585,7 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
                 if (h.type == T_FIXED) fixed_fused<CHK>(b, rs.k, row, hh, h.order, h.wasted, limit, trunc);
                 else if (MAXW == 8 && h.path == P_MMX16) lpc_fused<CHK, 8, P_MMX16>(b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
                 else if (MAXW == 8) lpc_fused<CHK, 8, P_IA32>(b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
-                else LPC_DISPATCH(lpc_fused, W, b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
+                else LPC_DISPATCH(lpc_fused, b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
                 rs.left -= CHK;
             } else {
                 STAT(b.stats, 1);
@@ -1504,7 +1606,7 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
                 } else if (h.type == T_FIXED) {
                     fixed_chunk<CHK>(row, hh, n0, nvalid, h.order, h.wasted);
                 } else {
-                    LPC_DISPATCH(lpc_chunk, W, row, c, hh, ht, n0, nvalid, h.order, sh, h.wasted);
+                    LPC_DISPATCH(lpc_chunk, row, c, hh, ht, n0, nvalid, h.order, sh, h.wasted);
                 }
             }
         }
@@ -1521,35 +1623,31 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : 1) k_decode(const u
         const uint64_t tc = tnow(tmon);
         tm_dec += tb - ta;
         tm_ref += tc - tb;
-        uint32_t pk = 0, pkn = 0;
+        uint32_t pk = 0;
         switch ((ablate & 2u) ? -1 : fmt) {
         case -1:
             break;
         case BNF_OUT_PLANAR32:
             pk = pack_lane<BNF_OUT_PLANAR32, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
-            pkn = pack_fast_stores<BNF_OUT_PLANAR32, CHK>();
             break;
         case BNF_OUT_INTERLEAVED32:
             pk = pack_lane<BNF_OUT_INTERLEAVED32, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
-            pkn = pack_fast_stores<BNF_OUT_INTERLEAVED32, CHK>();
             break;
         case BNF_OUT_FLACDECODER:
             pk = pack_lane<BNF_OUT_FLACDECODER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
-            pkn = pack_fast_stores<BNF_OUT_FLACDECODER, CHK>();
             break;
         default:
             pk = pack_lane<BNF_OUT_FILEREADER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels,
                                                     sp.bps == 24 ? 3u : 2u, out);
-            pkn = pack_fast_stores<BNF_OUT_FILEREADER, CHK>();
             break;
         }
-        /* account this chunk's stores for the next refill's exact vmcnt wait: the vector
-         * path issues a fixed count; after the per-sample path, drain (rare) */
-        if (__any(pk == 2u)) {
-            wait_vm();
-            br_drained(b);
-        } else if (__any(pk == 1u)) {
-            vq.s_last += pkn;
+        /* account this chunk's stores for the next refill's counted vmcnt wait: the wave
+         * issued at least the store count of every lane that stored (a lower bound keeps
+         * the wait exact or conservative) */
+        {
+            uint32_t m = pk ? pk : 0xFFFFFFFFu;
+            for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+            vq.s_last += (m == 0xFFFFFFFFu) ? 0u : m;
         }
         lds_sync();
         tm_pack += tnow(tmon) - tc;
@@ -2561,8 +2659,8 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
 #define TU_FN(name) TU_FN2(name, BNF_TU)
 #define TU_FN2(name, n) TU_FN3(name, n)
 #define TU_FN3(name, n) name##_tu##n
-#if BNF_TU == 1 || BNF_TU == 2
-#define DEC_W (BNF_TU == 1 ? 8 : 32)
+#if BNF_TU == 1 || BNF_TU == 2 || BNF_TU == 5
+#define DEC_W (BNF_TU == 1 ? 8 : (BNF_TU == 5 ? 16 : 32))
 extern "C" {
 hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     return upload_tables(crc8, crc16x8, xpow);
@@ -2649,6 +2747,11 @@ hipError_t bnf_launch_decode_tu3(const uint32_t *, uint64_t, uint32_t, bnf_strea
                                  uint64_t, bnf_frame_info *, hipStream_t);
 hipError_t bnf_launch_decode_tu4(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
                                  uint64_t, bnf_frame_info *, hipStream_t);
+hipError_t bnf_upload_tables_tu5(const uint8_t *, const uint16_t *, const uint16_t *);
+void bnf_set_ablate_tu5(uint32_t);
+hipError_t bnf_stats_tu5(uint64_t *, int);
+hipError_t bnf_launch_decode_tu5(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                 uint64_t, bnf_frame_info *, hipStream_t);
 hipError_t bnf_upload_tables_tu1(const uint8_t *, const uint16_t *, const uint16_t *);
 hipError_t bnf_upload_tables_tu2(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu1(uint32_t);
@@ -2666,6 +2769,7 @@ hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const
     if (e == hipSuccess) e = bnf_upload_tables_tu2(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu3(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu4(crc8, crc16x8, xpow);
+    if (e == hipSuccess) e = bnf_upload_tables_tu5(crc8, crc16x8, xpow);
     return e;
 }
 
@@ -2691,6 +2795,7 @@ void bnf_set_ablate(uint32_t v) {
     bnf_set_ablate_tu2(v);
     bnf_set_ablate_tu3(v);
     bnf_set_ablate_tu4(v);
+    bnf_set_ablate_tu5(v);
 }
 
 hipError_t bnf_stats(uint64_t *out16, int reset) {
@@ -2698,6 +2803,7 @@ hipError_t bnf_stats(uint64_t *out16, int reset) {
     hipError_t e = bnf_stats_tu1(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu2(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu3(out16, reset);
+    if (e == hipSuccess) e = bnf_stats_tu5(out16, reset);
     return e == hipSuccess ? bnf_stats_tu4(out16, reset) : e;
 }
 
@@ -2721,6 +2827,7 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
                        ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s)
                        : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
     if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
     if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
     return e;
 }

@@ -1,0 +1,11 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/pytest_r2e.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_r2e.log
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-reader --no-index --out gpurun_out/bench_r2e.json > gpurun_out/bench_r2e.log 2>&1; echo "bench rc=$?"
+python - <<'PY'
+import json
+d=json.loads(open('gpurun_out/bench_r2e.json').read())
+print('C2', d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['bitexact'])
+for k,v in d.get('legs',{}).items(): print(k, v['value'], v['roofline']['avg_launch_ms'], v['roofline']['k_parse_avg_ms'], v['roofline']['frac'], v['bitexact'])
+PY
