@@ -362,8 +362,11 @@ struct FLAC__StreamDecoder {
     FILE *file = nullptr;
     bool ignore_write_status = false;
 
-    /* every byte delivered by the read callback; pos = consumed */
+    /* bytes delivered by the read callback, stream offsets [buf_base, buf_base + buf.size());
+     * pos = consumed (absolute).  Bytes below the frame being decoded are dropped once they
+     * pile up (trim_consumed); a seek repositions the client and restarts the buffer there. */
     std::vector<uint8_t> buf;
+    uint64_t buf_base = 0;
     uint64_t pos = 0;
     uint64_t bitpos_meta = 0; /* bit cursor used while reading metadata */
     bool cached = false;
@@ -402,12 +405,31 @@ struct FLAC__StreamDecoder {
     std::vector<uint64_t> cand;
     std::vector<bnf_frame_info> info;
     std::vector<int32_t> pcm;
-    uint64_t read_ahead = 32ull << 20;
+    uint32_t pcm_ch = 1;                    /* planar slots per sample in pcm: the window's widest frame */
+    uint64_t read_ahead = 32ull << 20;      /* window read-ahead cap */
+    uint64_t read_ahead_cur = 256ull << 10; /* grows x2 per window up to the cap: the first frame comes quickly */
 };
 
 namespace {
 
 using Dec = FLAC__StreamDecoder;
+
+uint64_t bend(const Dec *d) { return d->buf_base + d->buf.size(); } /* one past the last buffered byte */
+uint8_t bat(const Dec *d, uint64_t p) { return d->buf[(size_t)(p - d->buf_base)]; }
+
+/* The caller's current HIP device is restored on scope exit (the library never leaves the
+ * thread on another device). */
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DevGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
 
 /* read_callback_ (stream_decoder.c) semantics, without touching the decoder state:
  * 0 = got bytes, 1 = end of stream, 2 = abort. */
@@ -437,7 +459,7 @@ int fill_raw(Dec *d, size_t want = 65536) {
 
 /* the decoder genuinely needs bytes [.., upto): failure sets END_OF_STREAM / ABORTED */
 bool need_bytes(Dec *d, uint64_t upto) {
-    while (d->buf.size() < upto) {
+    while (bend(d) < upto) {
         int r = fill_raw(d);
         if (r) {
             if (!d->client_done) d->client_done = r;
@@ -450,7 +472,7 @@ bool need_bytes(Dec *d, uint64_t upto) {
 
 /* read ahead for the GPU window; hitting the client's end is remembered, not reported */
 void read_ahead(Dec *d, uint64_t upto) {
-    while (d->buf.size() < upto && !d->client_done) {
+    while (bend(d) < upto && !d->client_done) {
         int r = fill_raw(d);
         if (r) d->client_done = r;
     }
@@ -465,7 +487,7 @@ bool mb_read(Dec *d, uint32_t *v, unsigned bits) {
     uint64_t end = d->bitpos_meta + bits;
     if (!need_bytes(d, (end + 7) / 8)) return false;
     uint64_t x = 0;
-    for (uint64_t p = d->bitpos_meta; p < end; p++) x = (x << 1) | ((d->buf[p >> 3] >> (7 - (p & 7))) & 1u);
+    for (uint64_t p = d->bitpos_meta; p < end; p++) x = (x << 1) | ((bat(d, p >> 3) >> (7 - (p & 7))) & 1u);
     d->bitpos_meta = end;
     *v = (uint32_t)x;
     return true;
@@ -599,8 +621,19 @@ bool read_metadata(Dec *d) {
 
 bool byte_at(Dec *d, uint64_t p, uint32_t *x) {
     if (!need_bytes(d, p + 1)) return false;
-    *x = d->buf[p];
+    *x = bat(d, p);
     return true;
+}
+
+/* Drop consumed bytes once they pile up: everything below `keep` (the frame being decoded)
+ * is no longer needed -- decoded windows live on the GPU and in info/pcm, and a seek
+ * refills through the client's seek callback. */
+void trim_consumed(Dec *d, uint64_t keep) {
+    if (keep <= d->buf_base) return;
+    const uint64_t drop = std::min<uint64_t>(keep - d->buf_base, d->buf.size());
+    if (drop < (16ull << 20) || drop * 2 < d->buf.size()) return;
+    d->buf.erase(d->buf.begin(), d->buf.begin() + (ptrdiff_t)drop);
+    d->buf_base += drop;
 }
 
 /* frame_sync_ (@0x10011760) over the host buffer */
@@ -643,8 +676,11 @@ bool frame_sync(Dec *d) {
 bool gpu_init(Dec *d) {
     if (d->gpu_ready) return true;
     const char *dev = getenv("BNFLAC_DEVICE");
-    d->device = dev ? atoi(dev) : 0;
+    int cur = 0;
+    if (!dev && hipGetDevice(&cur) != hipSuccess) cur = 0;
+    d->device = dev ? atoi(dev) : cur; /* the caller's device (a torchrun rank's), unless overridden */
     if (bnflac_ctx_create(d->device, &d->ctx) != 0) return false;
+    DevGuard g(d->device);
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) return fail("bnflac: stream create failed") == 0;
     d->gpu_ready = true;
     return true;
@@ -652,7 +688,7 @@ bool gpu_init(Dec *d) {
 
 void gpu_free(Dec *d) {
     if (!d->gpu_ready) return;
-    (void)hipSetDevice(d->device);
+    DevGuard g(d->device);
     d->d_bytes.release();
     d->d_cand.release();
     d->d_count.release();
@@ -671,12 +707,12 @@ bool decode_window(Dec *d, uint64_t base) {
         d->state = FLAC__STREAM_DECODER_MEMORY_ALLOCATION_ERROR;
         return false;
     }
-    (void)hipSetDevice(d->device);
-    const uint64_t n = d->buf.size() - base;
+    DevGuard g(d->device);
+    const uint64_t n = bend(d) - base;
     const size_t padded = (size_t)((n + 3) & ~3ull) + 16;
     if (!d->d_bytes.grow(padded)) goto oom;
     if (hipMemsetAsync((uint8_t *)d->d_bytes.p + (n & ~3ull), 0, padded - (n & ~3ull), d->stream) != hipSuccess) goto hip_fail;
-    if (hipMemcpyAsync(d->d_bytes.p, d->buf.data() + base, n, hipMemcpyHostToDevice, d->stream) != hipSuccess) goto hip_fail;
+    if (hipMemcpyAsync(d->d_bytes.p, d->buf.data() + (base - d->buf_base), n, hipMemcpyHostToDevice, d->stream) != hipSuccess) goto hip_fail;
     {
         uint32_t cap = (uint32_t)std::min<uint64_t>(n / 2 + 16, 1u << 30);
         cap = std::min<uint32_t>(cap, (uint32_t)(n / 64 + 4096));
@@ -712,7 +748,6 @@ bool decode_window(Dec *d, uint64_t base) {
                 sp.bps = si.bits_per_sample;
                 sp.total_samples = si.total_samples;
             }
-            const uint32_t pcm_ch = 8; /* planar slots sized for any channel count */
             if (!d->d_info.grow(sizeof(bnf_frame_info) * ncand)) goto oom;
             if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, n, (const uint64_t *)d->d_cand.p, ncand, sp,
                                  nullptr, 0, (bnf_frame_info *)d->d_info.p, 0, d->stream) != hipSuccess)
@@ -721,16 +756,21 @@ bool decode_window(Dec *d, uint64_t base) {
                 goto hip_fail;
             if (hipStreamSynchronize(d->stream) != hipSuccess) goto hip_fail;
             uint64_t tot = 0;
+            uint32_t pcm_ch = 1; /* planar slots per sample: the window's widest frame */
             for (auto &fi : d->info) {
                 fi.out_sample = tot;
-                if (fi.status == BNF_ST_OK) tot += fi.blocksize;
+                if (fi.status == BNF_ST_OK) {
+                    tot += fi.blocksize;
+                    pcm_ch = std::max(pcm_ch, std::min<uint32_t>(fi.channels, 8u));
+                }
             }
+            d->pcm_ch = pcm_ch;
             if (!d->d_pcm.grow(sizeof(int32_t) * (size_t)std::max<uint64_t>(tot, 1) * pcm_ch)) goto oom;
             if (hipMemcpyAsync(d->d_info.p, d->info.data(), sizeof(bnf_frame_info) * ncand, hipMemcpyHostToDevice, d->stream) != hipSuccess)
                 goto hip_fail;
             bnf_stream_params spd = sp;
             spd.channels = pcm_ch;
-            if (bnf_launch_decode((const uint32_t *)d->d_bytes.p, n, ncand, spd, 8, BNF_OUT_PLANAR32,
+            if (bnf_launch_decode((const uint32_t *)d->d_bytes.p, n, ncand, spd, lanes_for(pcm_ch), BNF_OUT_PLANAR32,
                                   (uint8_t *)d->d_pcm.p, (uint64_t)std::max<uint64_t>(tot, 1) * pcm_ch * 4,
                                   (bnf_frame_info *)d->d_info.p, d->stream) != hipSuccess)
                 goto hip_fail;
@@ -743,8 +783,9 @@ bool decode_window(Dec *d, uint64_t base) {
         }
     }
     d->win_base = base;
-    d->win_end = d->buf.size();
+    d->win_end = bend(d);
     d->win_valid = true;
+    d->read_ahead_cur = std::min(d->read_ahead, d->read_ahead_cur * 2);
     return true;
 oom:
     fail("bnflac: out of device memory");
@@ -788,13 +829,13 @@ bool read_frame(Dec *d, bool *got) {
         if (d->client_done) {
             /* no more bytes will come: a truncated frame makes libFLAC's reader fail here */
             if ((fi && fi->status == BNF_ST_TRUNC) ||
-                (d->win_valid && d->win_base == p && d->win_end == d->buf.size())) {
-                need_bytes(d, d->buf.size() + 1);
+                (d->win_valid && d->win_base == p && d->win_end == bend(d))) {
+                need_bytes(d, bend(d) + 1);
                 return false;
             }
         } else {
-            const uint64_t have = d->buf.size() > p ? d->buf.size() - p : 0;
-            read_ahead(d, p + std::max<uint64_t>(d->read_ahead, 2 * have + 4096));
+            const uint64_t have = bend(d) > p ? bend(d) - p : 0;
+            read_ahead(d, p + std::max<uint64_t>(d->read_ahead_cur, 2 * have + 4096));
         }
         if (!decode_window(d, p)) return false;
     }
@@ -861,7 +902,7 @@ bool read_frame(Dec *d, bool *got) {
     }
     d->frame.footer.crc = (FLAC__uint16)fi->crc16_read;
     allocate_output(d, h.blocksize, h.channels);
-    const int32_t *src = d->pcm.data() + (size_t)fi->out_sample * 8;
+    const int32_t *src = d->pcm.data() + (size_t)fi->out_sample * d->pcm_ch;
     for (unsigned c = 0; c < h.channels; c++)
         memcpy(d->output[c].data(), src + (size_t)c * h.blocksize, sizeof(int32_t) * h.blocksize);
     if (!fi->crc_ok) send_error(d, FLAC__STREAM_DECODER_ERROR_STATUS_FRAME_CRC_MISMATCH); /* output already zeroed */
@@ -874,6 +915,7 @@ bool read_frame(Dec *d, bool *got) {
     d->blocksize = h.blocksize;
     d->samples_decoded = h.number.sample_number + h.blocksize;
     d->pos = abs_resume / 8;
+    trim_consumed(d, p);
     const FLAC__int32 *bufs[FLAC__MAX_CHANNELS];
     for (unsigned c = 0; c < FLAC__MAX_CHANNELS; c++) bufs[c] = c < d->output_channels ? d->output[c].data() : nullptr;
     if (d->is_seeking) {
@@ -888,10 +930,14 @@ bool read_frame(Dec *d, bool *got) {
             const FLAC__int32 *nb[FLAC__MAX_CHANNELS];
             for (unsigned c = 0; c < FLAC__MAX_CHANNELS; c++) nb[c] = bufs[c] ? bufs[c] + delta : nullptr;
             d->is_seeking = false;
+            /* the callback runs in READ_FRAME, as libFLAC's; it may itself seek again */
+            FLAC__StreamDecoderWriteStatus ws = d->write_cb(d, &fr, nb, d->client);
+            if (ws != FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE && !d->ignore_write_status) {
+                d->seek_done = -1;
+                return false; /* state stays READ_FRAME */
+            }
             d->seek_done = 1;
             d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
-            FLAC__StreamDecoderWriteStatus ws = d->write_cb(d, &fr, nb, d->client);
-            if (ws != FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE && !d->ignore_write_status) d->seek_done = -1;
             return true;
         }
         d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
@@ -908,6 +954,7 @@ bool read_frame(Dec *d, bool *got) {
 
 void reset_fields(Dec *d) {
     d->buf.clear();
+    d->buf_base = 0;
     d->pos = 0;
     d->bitpos_meta = 0;
     d->cached = false;
@@ -922,7 +969,99 @@ void reset_fields(Dec *d) {
     d->pcm.clear();
     d->is_seeking = false;
     d->do_md5 = d->md5_checking;
+    d->read_ahead_cur = std::min<uint64_t>(d->read_ahead, 256ull << 10);
     md5_init(d->md5);
+}
+
+/* Sample number of a decoded window frame (the header number conversion of read_frame). */
+uint64_t frame_first_sample(const Dec *d, const bnf_frame_info &fi) {
+    if (fi.number_type == 1) return fi.number;
+    if (d->fixed_block_size) return (uint64_t)d->fixed_block_size * fi.number;
+    if (d->has_stream_info) {
+        const FLAC__StreamMetadata_StreamInfo &si = d->stream_info.data.stream_info;
+        if (si.min_blocksize == si.max_blocksize) return (uint64_t)si.min_blocksize * fi.number;
+    }
+    return (uint64_t)fi.blocksize * fi.number;
+}
+
+/* Frame of the decoded window that holds `target` (intact frames only: header, CRC-16).
+ * Returns 1 found (*off = its absolute offset), 0 the window's frames all lie before it
+ * (lo_off/lo_s = the last one), -1 they all lie after it (hi_off/hi_s = the first one),
+ * -2 the window has no intact frame. */
+int window_find(const Dec *d, uint64_t target, uint64_t *off, uint64_t *lo_off, uint64_t *lo_s, uint64_t *hi_off,
+                uint64_t *hi_s) {
+    bool any = false;
+    uint64_t f_off = 0, f_s = 0, l_off = 0, l_s = 0;
+    for (size_t i = 0; i < d->info.size(); i++) {
+        const bnf_frame_info &fi = d->info[i];
+        if (fi.status != BNF_ST_OK || !fi.crc_ok) continue;
+        const uint64_t sn = frame_first_sample(d, fi), o = d->win_base + d->cand[i];
+        if (sn <= target && target < sn + fi.blocksize) {
+            *off = o;
+            return 1;
+        }
+        if (!any) { f_off = o; f_s = sn; }
+        l_off = o;
+        l_s = sn + fi.blocksize;
+        any = true;
+    }
+    if (!any) return -2;
+    if (target < f_s) { *hi_off = f_off; *hi_s = f_s; return -1; }
+    *lo_off = l_off;
+    *lo_s = l_s;
+    return 0;
+}
+
+/* Reposition the client at `at` and decode one window from there. */
+bool window_at(Dec *d, uint64_t at, uint64_t bytes) {
+    if (d->seek_cb(d, at, d->client) != FLAC__STREAM_DECODER_SEEK_STATUS_OK) return false;
+    d->buf.clear();
+    d->buf_base = at;
+    d->client_done = 0;
+    d->win_valid = false;
+    d->cached = false;
+    read_ahead(d, at + bytes);
+    if (bend(d) <= at) return false;
+    return decode_window(d, at);
+}
+
+/* Byte offset of the frame holding `target`: the current window when it is there and its
+ * bytes are still buffered; otherwise an interpolation search between known (offset,
+ * sample) points, each probe one client seek + one GPU window (O(window) per probe,
+ * O(log) probes), like libFLAC's seek_to_absolute_sample_ but over decoded windows. */
+bool seek_position(Dec *d, uint64_t target, uint64_t length, uint64_t *start) {
+    uint64_t off = 0, lo_off = d->first_frame_offset, lo_s = 0, hi_off = length, hi_s = 0;
+    if (d->win_valid && window_find(d, target, &off, &lo_off, &lo_s, &hi_off, &hi_s) == 1 && off >= d->buf_base) {
+        *start = off;
+        return true;
+    }
+    const FLAC__uint64 total = FLAC__stream_decoder_get_total_samples(d);
+    lo_off = d->first_frame_offset;
+    lo_s = 0;
+    hi_off = length;
+    hi_s = total ? total : ~0ull;
+    const uint32_t maxfs = d->has_stream_info ? d->stream_info.data.stream_info.max_framesize : 0;
+    const uint64_t win = std::max<uint64_t>(1ull << 20, 4ull * (maxfs ? maxfs : 65536));
+    for (int probe = 0; probe < 64; probe++) {
+        if (hi_off <= lo_off) return false;
+        uint64_t est = lo_off;
+        if (hi_s != ~0ull && hi_s > lo_s && target > lo_s)
+            est = lo_off + (uint64_t)((double)(target - lo_s) / (double)(hi_s - lo_s) * (double)(hi_off - lo_off));
+        est = (est > lo_off + win / 2) ? est - win / 2 : lo_off; /* aim the window's middle at the target */
+        if (!window_at(d, est, win)) return false;
+        const int r = window_find(d, target, &off, &lo_off, &lo_s, &hi_off, &hi_s);
+        if (r == 1) {
+            *start = off;
+            return true;
+        }
+        if (r == -2) { /* nothing intact here: shrink the range from above */
+            if (est == lo_off) return false;
+            hi_off = est;
+        } else if (r == -1 && est <= lo_off) {
+            return false; /* the first frame at/after the range start is already past the target */
+        }
+    }
+    return false;
 }
 
 /* file callbacks (stream_decoder.c file_*_callback_) */
@@ -1126,25 +1265,44 @@ BNFLAC_API FLAC__bool FLAC__stream_decoder_process_until_end_of_stream(FLAC__Str
 }
 
 BNFLAC_API FLAC__bool FLAC__stream_decoder_seek_absolute(FLAC__StreamDecoder *d, FLAC__uint64 sample) {
+    /* stream_decoder.c FLAC__stream_decoder_seek_absolute: states 0-4, a seek callback, the
+     * target below STREAMINFO's total; is_seeking and MD5-off come BEFORE the metadata pass
+     * (a seek before it suppresses the STREAMINFO callback), then the length callback. */
     if (!d) return 0;
     if (d->state > FLAC__STREAM_DECODER_END_OF_STREAM) return 0;
     if (!d->seek_cb) return 0;
     FLAC__uint64 total = FLAC__stream_decoder_get_total_samples(d);
     if (total > 0 && sample >= total) return 0;
-    FLAC__uint64 length = 0;
-    if (d->length_cb(d, &length, d->client) != FLAC__STREAM_DECODER_LENGTH_STATUS_OK) return 0;
-    if (d->state <= FLAC__STREAM_DECODER_READ_METADATA) {
-        if (!FLAC__stream_decoder_process_until_end_of_metadata(d)) return 0;
-        total = FLAC__stream_decoder_get_total_samples(d);
-        if (total > 0 && sample >= total) return 0;
-    }
-    /* Walk frames from the first frame (every byte read so far is still buffered) until
-     * the one holding `sample`; only that frame reaches the write callback, trimmed. */
-    d->do_md5 = false; /* a seek turns MD5 checking off (stream_decoder.c seek_absolute) */
     d->is_seeking = true;
+    d->do_md5 = false; /* a seek turns MD5 checking off */
+    FLAC__uint64 length = 0;
+    if (d->length_cb(d, &length, d->client) != FLAC__STREAM_DECODER_LENGTH_STATUS_OK) {
+        d->is_seeking = false;
+        return 0;
+    }
+    if (d->state <= FLAC__STREAM_DECODER_READ_METADATA) {
+        if (!FLAC__stream_decoder_process_until_end_of_metadata(d)) {
+            d->is_seeking = false;
+            return 0;
+        }
+        total = FLAC__stream_decoder_get_total_samples(d);
+        if (total > 0 && sample >= total) {
+            d->is_seeking = false;
+            return 0;
+        }
+    }
+    /* seek_to_absolute_sample_: find the frame holding `sample` (one decoded window when it
+     * is already there, else an interpolation search over client seeks, each step one GPU
+     * window), then decode from it: only that frame reaches the write callback, trimmed. */
+    uint64_t start = 0;
+    if (!seek_position(d, sample, length, &start)) {
+        d->is_seeking = false;
+        d->state = FLAC__STREAM_DECODER_SEEK_ERROR;
+        return 0;
+    }
     d->seek_target = sample;
     d->seek_done = 0;
-    d->pos = d->first_frame_offset;
+    d->pos = start;
     d->cached = false;
     d->samples_decoded = 0;
     d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
@@ -1167,7 +1325,7 @@ BNFLAC_API FLAC__bool FLAC__stream_decoder_seek_absolute(FLAC__StreamDecoder *d,
 BNFLAC_API FLAC__bool FLAC__stream_decoder_get_decode_position(const FLAC__StreamDecoder *d, FLAC__uint64 *position) {
     if (!d || !d->tell_cb) return 0;
     if (d->tell_cb(d, position, d->client) != FLAC__STREAM_DECODER_TELL_STATUS_OK) return 0;
-    const uint64_t unconsumed = d->buf.size() - std::min<uint64_t>(d->pos, d->buf.size());
+    const uint64_t unconsumed = bend(d) - std::min<uint64_t>(d->pos, bend(d));
     *position -= unconsumed;
     return 1;
 }

@@ -14,13 +14,21 @@ import numpy as np
 from .libflac import (LibFLAC, DecoderEofCallback, DecoderReadCallback, DecoderWriteCallbackWithStatus,
                       Decoder_ErrorCallback, Decoder_MetadataCallback, load)
 
-EV_METADATA, EV_WRITE, EV_ERROR, EV_RETURN = 1, 2, 3, 4
+EV_METADATA, EV_WRITE, EV_ERROR, EV_RETURN, EV_SEEK = 1, 2, 3, 4, 5
 
 
-def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: int = -1, md5_check: bool = False):
+def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: int = -1, md5_check: bool = False,
+        seeks=None, stats=None):
     """-> (events, pcm); with md5_check, MD5 checking is enabled before init and the
     result is (events, pcm, finish_ok) where finish_ok is FLAC__stream_decoder_finish's
-    return (false on an MD5 mismatch)."""
+    return (false on an MD5 mismatch).
+
+    seeks: FLACFileReader's seek pattern (FLACFileReader.cs:125-136, 267-301) as oracle.run_seek
+    drives it -- a list of (write_index | -1, target_sample): after copying write number
+    write_index the write callback itself calls seek_absolute (the trimmed target frame
+    arrives through a nested write callback); -1 seeks right after the metadata pass.  The
+    stream then has memory seek/tell/length callbacks, and every seek_absolute return is an
+    EV_SEEK event."""
     L = load()
     data = bytes(data)
     st = {"pos": 0, "eof": False, "frames": 0}
@@ -44,6 +52,7 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
         length = min(want, read_chunk)
         chunk = data[st["pos"]: st["pos"] + length]
         n = len(chunk)
+        st["read_total"] = st.get("read_total", 0) + n
         if n:
             ctypes.memmove(buf, chunk, n)
         st["pos"] += n
@@ -56,6 +65,30 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
     def eof(d, ud):
         return 1 if st["eof"] else 0
 
+    seeks = list(seeks or [])
+    nxt = [0]
+
+    def do_seek():
+        target = seeks[nxt[0]][1]
+        nxt[0] += 1
+        r = int(L.FLAC__stream_decoder_seek_absolute(dec, target))
+        events.append((EV_SEEK, r, state(), 0, 0, 0, 0, 0, 0, 0))
+
+    def sk(d, off, ud):
+        if off > len(data):
+            return 1
+        st["pos"] = int(off)
+        st["eof"] = False
+        return 0
+
+    def tl(d, off, ud):
+        off[0] = st["pos"]
+        return 0
+
+    def ln(d, n, ud):
+        n[0] = len(data)
+        return 0
+
     def wr(d, frame, buf, ud):
         raw = ctypes.string_at(frame, 40)
         bs, sr, ch, asg, bps, _nt = np.frombuffer(raw[:24], dtype="<u4")
@@ -66,6 +99,8 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
             npcm[0] += int(bs)
         idx = st["frames"]
         st["frames"] += 1
+        if nxt[0] < len(seeks) and seeks[nxt[0]][0] == idx:
+            do_seek()
         return 1 if idx == write_abort_at else 0
 
     def md(d, m, ud):
@@ -83,17 +118,27 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
     def er(d, status, ud):
         events.append((EV_ERROR, int(status), state(), 0, 0, 0, 0, 0, 0, 0))
 
+    from .libflac import DecoderSeekCallback, DecoderTellCallback, DecoderLengthCallback
     cbs = (DecoderReadCallback(rd), DecoderEofCallback(eof), DecoderWriteCallbackWithStatus(wr),
-           Decoder_MetadataCallback(md), Decoder_ErrorCallback(er))
-    rc = L.FLAC__stream_decoder_init_stream(dec, cbs[0], _null(0), _null(1), _null(2), cbs[1], cbs[2], cbs[3],
-                                            cbs[4], None)
+           Decoder_MetadataCallback(md), Decoder_ErrorCallback(er), DecoderSeekCallback(sk), DecoderTellCallback(tl),
+           DecoderLengthCallback(ln))
+    if seeks:
+        rc = L.FLAC__stream_decoder_init_stream(dec, cbs[0], cbs[5], cbs[6], cbs[7], cbs[1], cbs[2], cbs[3], cbs[4],
+                                                None)
+    else:
+        rc = L.FLAC__stream_decoder_init_stream(dec, cbs[0], _null(0), _null(1), _null(2), cbs[1], cbs[2], cbs[3],
+                                                cbs[4], None)
     if rc != 0:
         L.FLAC__stream_decoder_delete(dec)
         raise RuntimeError(f"init_stream failed rc={rc}: {L.bnflac_last_error().decode()}")
     try:
+        while nxt[0] < len(seeks) and seeks[nxt[0]][0] == -2:  # right after init: before the metadata pass
+            do_seek()
         if driver == 0:
             ok = int(L.FLAC__stream_decoder_process_until_end_of_metadata(dec))
             events.append((EV_RETURN, ok, state(), 0, 0, 0, 0, 0, 0, 0))
+            while ok and nxt[0] < len(seeks) and seeks[nxt[0]][0] < 0:
+                do_seek()
             if ok:
                 for _ in range(50_000_000):
                     if state() >= 4:
@@ -109,6 +154,8 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
             finish_ok = bool(L.FLAC__stream_decoder_finish(dec))
     finally:
         L.FLAC__stream_decoder_delete(dec)
+    if stats is not None:
+        stats["read_total"] = st.get("read_total", 0)
     pcm = np.concatenate(pcm_parts) if pcm_parts else np.zeros(0, dtype=np.int32)
     if md5_check:
         return events, pcm, finish_ok

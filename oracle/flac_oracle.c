@@ -91,6 +91,10 @@ struct oracle_decoder {
     unsigned rice_raw[FLAC__MAX_CHANNELS][1u << 15];
     FLAC__EntropyCodingMethod_PartitionedRiceContents rice_contents[FLAC__MAX_CHANNELS];
 
+    /* seeking (seek_absolute / seek_to_absolute_sample_) */
+    int is_seeking;
+    uint64_t first_frame_offset, target_sample;
+
     /* FLAC__StreamDecoderProtected */
     unsigned channels, bits_per_sample, sample_rate, blocksize;
     FLAC__ChannelAssignment channel_assignment;
@@ -302,8 +306,8 @@ static int br_utf8_u64(oracle_decoder *d, uint64_t *val, uint8_t *raw, unsigned 
     return 1;
 }
 
-static void send_error(oracle_decoder *d, FLAC__StreamDecoderErrorStatus st) {
-    if (d->error_cb) d->error_cb((const FLAC__StreamDecoder *)d, st, d->client);
+static void send_error(oracle_decoder *d, FLAC__StreamDecoderErrorStatus st) { /* send_error_to_client_ */
+    if (d->error_cb && !d->is_seeking) d->error_cb((const FLAC__StreamDecoder *)d, st, d->client);
 }
 
 /* ------------------------------------------------------------------ restore kernels */
@@ -855,10 +859,27 @@ static int read_frame(oracle_decoder *d, int *got_frame, int *crc_ok_out) {
     d->blocksize = d->frame.header.blocksize;
     d->samples_decoded = d->frame.header.number.sample_number + d->frame.header.blocksize;
     /* write_audio_frame_to_client_ @0x100131e0; a non-CONTINUE return makes read_frame_
-     * return false WITHOUT touching the state (@0x10011bd3-0x10011be4). */
-    if (d->write_cb((const FLAC__StreamDecoder *)d, &d->frame, (const int32_t *const *)d->output, d->client) !=
-        FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE)
-        return 0;
+     * return false WITHOUT touching the state (@0x10011bd3-0x10011be4).  While seeking,
+     * only the frame holding the target sample reaches the client, with the samples before
+     * the target shifted out (blocksize and sample number adjusted); it ends seek mode. */
+    FLAC__StreamDecoderWriteStatus ws = FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE;
+    if (d->is_seeking) {
+        const uint64_t sn = d->frame.header.number.sample_number, next = sn + d->frame.header.blocksize;
+        if (sn <= d->target_sample && d->target_sample < next) {
+            const unsigned delta = (unsigned)(d->target_sample - sn);
+            d->is_seeking = 0;
+            FLAC__Frame last = d->frame;
+            const int32_t *nb[FLAC__MAX_CHANNELS];
+            for (unsigned ch = 0; ch < FLAC__MAX_CHANNELS; ch++)
+                nb[ch] = ch < d->frame.header.channels ? d->output[ch] + delta : NULL;
+            last.header.blocksize -= delta;
+            last.header.number.sample_number += delta;
+            ws = d->write_cb((const FLAC__StreamDecoder *)d, &last, nb, d->client);
+        }
+    } else {
+        ws = d->write_cb((const FLAC__StreamDecoder *)d, &d->frame, (const int32_t *const *)d->output, d->client);
+    }
+    if (ws != FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE) return 0;
     d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
     return 1;
 }
@@ -992,13 +1013,16 @@ static int read_metadata(oracle_decoder *d) {
         if (!br_read_bytes(d, si->md5sum, 16)) return 0;
         if (!br_skip_bytes(d, length - 34u)) return 0; /* unsigned, as libFLAC */
         d->has_stream_info = 1;
-        if (d->metadata_cb) d->metadata_cb((const FLAC__StreamDecoder *)d, m, d->client);
+        if (d->metadata_cb && !d->is_seeking) d->metadata_cb((const FLAC__StreamDecoder *)d, m, d->client);
     } else {
         /* SEEKTABLE is parsed by libFLAC for seeking only; other blocks are filtered out
          * by the default metadata_respond set (only STREAMINFO is reported). */
         if (!br_skip_bytes(d, length)) return 0;
     }
-    if (last) d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+    if (last) {
+        d->first_frame_offset = (uint64_t)(d->bitpos >> 3);
+        d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+    }
     return 1;
 }
 
@@ -1016,6 +1040,8 @@ static void reset_state(oracle_decoder *d) {
     d->has_stream_info = 0;
     d->samples_decoded = 0;
     d->fixed_block_size = d->next_fixed_block_size = 0;
+    d->is_seeking = 0;
+    d->first_frame_offset = 0;
     d->state = FLAC__STREAM_DECODER_SEARCH_FOR_METADATA;
 }
 
@@ -1122,6 +1148,57 @@ FLAC__bool oracle_process_until_end_of_stream(oracle_decoder *d) {
             return 0;
         }
     }
+}
+
+/* FLAC__stream_decoder_seek_absolute (libFLAC 1.2.1 stream_decoder.c): states 0-4 only,
+ * needs the seek callback, target below STREAMINFO's total; is_seeking and MD5-off are set
+ * BEFORE the metadata pass (so a seek issued before it suppresses the STREAMINFO callback),
+ * the length callback must answer.  seek_to_absolute_sample_ then repositions the client
+ * and decodes (errors suppressed, nothing delivered) until the frame holding the target,
+ * which write_audio_frame_to_client_ delivers trimmed (read_frame above).  The oracle keeps
+ * every byte it has read, so its repositioning is a restart of the bit reader at the first
+ * frame (the observable callbacks are libFLAC's: only the trimmed target frame); a failed
+ * search leaves SEEK_ERROR. */
+FLAC__bool oracle_seek_absolute(oracle_decoder *d, FLAC__uint64 sample) {
+    if (d->state > FLAC__STREAM_DECODER_END_OF_STREAM) return 0;
+    if (!d->seek_cb) return 0;
+    if (oracle_get_total_samples(d) > 0 && sample >= oracle_get_total_samples(d)) return 0;
+    d->is_seeking = 1;
+    FLAC__uint64 length = 0;
+    if (d->length_cb((const FLAC__StreamDecoder *)d, &length, d->client) != FLAC__STREAM_DECODER_LENGTH_STATUS_OK) {
+        d->is_seeking = 0;
+        return 0;
+    }
+    if (d->state <= FLAC__STREAM_DECODER_READ_METADATA) {
+        if (!oracle_process_until_end_of_metadata(d)) {
+            d->is_seeking = 0;
+            return 0;
+        }
+        if (oracle_get_total_samples(d) > 0 && sample >= oracle_get_total_samples(d)) {
+            d->is_seeking = 0;
+            return 0;
+        }
+    }
+    /* FLAC__stream_decoder_flush + reposition at the first frame */
+    d->target_sample = sample;
+    d->bitpos = (uint64_t)d->first_frame_offset * 8u;
+    d->cached = 0;
+    d->samples_decoded = 0;
+    d->state = FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC;
+    for (uint64_t guard = 0; guard < 100000000u && d->is_seeking; guard++) {
+        int got;
+        if (d->state == FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC) {
+            if (!frame_sync(d)) break;
+        } else if (d->state == FLAC__STREAM_DECODER_READ_FRAME) {
+            if (!read_frame(d, &got, NULL)) break; /* incl. ABORT from the target frame's write */
+        } else {
+            break;
+        }
+    }
+    if (!d->is_seeking && d->state == FLAC__STREAM_DECODER_SEARCH_FOR_FRAME_SYNC) return 1;
+    d->is_seeking = 0;
+    d->state = FLAC__STREAM_DECODER_SEEK_ERROR;
+    return 0;
 }
 
 FLAC__StreamDecoderState oracle_get_state(const oracle_decoder *d) { return d->state; }
@@ -1260,6 +1337,83 @@ int oracle_run(const uint8_t *data, size_t len, int driver, int read_chunk, int 
     }
     *n_ev = c.n_ev;
     *n_pcm = c.n_pcm;
+    oracle_delete(d);
+    return 0;
+}
+
+/* FLACFileReader's seek pattern (FLACFileReader.cs:125-136, 267-301): Position set ->
+ * the NEXT write callback copies its frame, then calls seek_absolute from inside itself;
+ * the trimmed target frame arrives through a nested write callback.  seeks[2i] is the write
+ * index (0-based) after which seek i is issued (-1: right after the metadata pass, before
+ * any frame; -2: right after init, before the metadata pass), seeks[2i+1] the target sample.  Events as oracle_run; every seek_absolute
+ * return is an ORACLE_EV_SEEK event.  Memory client with seek/tell/length callbacks. */
+typedef struct {
+    mem_client mc;
+    const int64_t *seeks;
+    int nseeks, next;
+} seek_client;
+
+static FLAC__StreamDecoderSeekStatus mem_seek(const FLAC__StreamDecoder *dec, FLAC__uint64 off, void *cd) {
+    (void)dec;
+    mem_client *c = (mem_client *)cd;
+    if (off > c->len) return FLAC__STREAM_DECODER_SEEK_STATUS_ERROR;
+    c->pos = (size_t)off;
+    c->hit_eof = 0;
+    return FLAC__STREAM_DECODER_SEEK_STATUS_OK;
+}
+static FLAC__StreamDecoderTellStatus mem_tell(const FLAC__StreamDecoder *dec, FLAC__uint64 *off, void *cd) {
+    (void)dec;
+    *off = ((mem_client *)cd)->pos;
+    return FLAC__STREAM_DECODER_TELL_STATUS_OK;
+}
+static FLAC__StreamDecoderLengthStatus mem_length(const FLAC__StreamDecoder *dec, FLAC__uint64 *len, void *cd) {
+    (void)dec;
+    *len = ((mem_client *)cd)->len;
+    return FLAC__STREAM_DECODER_LENGTH_STATUS_OK;
+}
+
+static void do_seek(seek_client *sc, oracle_decoder *d) {
+    const int64_t target = sc->seeks[2 * sc->next + 1];
+    sc->next++;
+    FLAC__bool r = oracle_seek_absolute(d, (FLAC__uint64)target);
+    push_event(&sc->mc, ORACLE_EV_SEEK, r);
+}
+
+static FLAC__StreamDecoderWriteStatus sk_write(const FLAC__StreamDecoder *dec, const FLAC__Frame *f,
+                                               const FLAC__int32 *const buf[], void *cd) {
+    seek_client *sc = (seek_client *)cd;
+    const int idx = sc->mc.frames;
+    (void)ev_write(dec, f, buf, &sc->mc); /* copies the frame (counts it) */
+    if (sc->next < sc->nseeks && sc->seeks[2 * sc->next] == idx) do_seek(sc, sc->mc.dec);
+    return FLAC__STREAM_DECODER_WRITE_STATUS_CONTINUE;
+}
+
+int oracle_run_seek(const uint8_t *data, size_t len, int read_chunk, const int64_t *seeks, int nseeks,
+                    oracle_event *ev, int ev_cap, int *n_ev, int32_t *pcm, size_t pcm_cap, size_t *n_pcm) {
+    seek_client sc;
+    memset(&sc, 0, sizeof sc);
+    mem_client *c = &sc.mc;
+    c->data = data; c->len = len; c->chunk = read_chunk > 0 ? read_chunk : 16384;
+    c->ev = ev; c->ev_cap = ev_cap; c->pcm = pcm; c->pcm_cap = pcm_cap; c->abort_at = -1;
+    sc.seeks = seeks; sc.nseeks = nseeks;
+    oracle_decoder *d = oracle_new();
+    c->dec = d;
+    int rc = oracle_init_stream(d, mem_read, mem_seek, mem_tell, mem_length, mem_eof, sk_write, ev_meta, ev_error, &sc);
+    if (rc != 0) { oracle_delete(d); return -rc; }
+    while (sc.next < sc.nseeks && sc.seeks[2 * sc.next] == -2) do_seek(&sc, d); /* before the metadata pass */
+    int ok = oracle_process_until_end_of_metadata(d);
+    push_event(c, ORACLE_EV_RETURN, ok);
+    while (ok && sc.next < sc.nseeks && sc.seeks[2 * sc.next] < 0) do_seek(&sc, d);
+    if (ok) {
+        for (int guard = 0; guard < 50000000; guard++) {
+            if (d->state >= FLAC__STREAM_DECODER_END_OF_STREAM) break;
+            ok = oracle_process_single(d);
+            push_event(c, ORACLE_EV_RETURN, ok);
+            if (!ok) break;
+        }
+    }
+    *n_ev = c->n_ev;
+    *n_pcm = c->n_pcm;
     oracle_delete(d);
     return 0;
 }

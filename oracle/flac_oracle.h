@@ -50,6 +50,7 @@ FLAC__bool oracle_finish(oracle_decoder *d);
 FLAC__bool oracle_process_single(oracle_decoder *d);
 FLAC__bool oracle_process_until_end_of_metadata(oracle_decoder *d);
 FLAC__bool oracle_process_until_end_of_stream(oracle_decoder *d);
+FLAC__bool oracle_seek_absolute(oracle_decoder *d, FLAC__uint64 sample);
 FLAC__StreamDecoderState oracle_get_state(const oracle_decoder *d);
 FLAC__uint64 oracle_get_total_samples(const oracle_decoder *d);
 unsigned oracle_get_channels(const oracle_decoder *d);
@@ -58,7 +59,7 @@ unsigned oracle_get_sample_rate(const oracle_decoder *d);
 
 /* ---- test drivers ------------------------------------------------------------------ */
 
-enum { ORACLE_EV_METADATA = 1, ORACLE_EV_WRITE = 2, ORACLE_EV_ERROR = 3, ORACLE_EV_RETURN = 4 };
+enum { ORACLE_EV_METADATA = 1, ORACLE_EV_WRITE = 2, ORACLE_EV_ERROR = 3, ORACLE_EV_RETURN = 4, ORACLE_EV_SEEK = 5 };
 
 typedef struct {
     int32_t kind;        /* ORACLE_EV_* */
@@ -81,6 +82,12 @@ typedef struct {
 int oracle_run(const uint8_t *data, size_t len, int driver, int read_chunk, int write_abort_at,
                oracle_event *ev, int ev_cap, int *n_ev, int32_t *pcm, size_t pcm_cap,
                size_t *n_pcm);
+
+/* FLACFileReader's seek pattern: seek_absolute issued from inside the write callback after
+ * write seeks[2i] (-1: after the metadata pass), to sample seeks[2i+1]; a SEEK event carries
+ * each seek_absolute return.  See flac_oracle.c. */
+int oracle_run_seek(const uint8_t *data, size_t len, int read_chunk, const int64_t *seeks, int nseeks,
+                    oracle_event *ev, int ev_cap, int *n_ev, int32_t *pcm, size_t pcm_cap, size_t *n_pcm);
 
 /* One frame, decoded as read_frame_ would after frame_sync_ matched at byte `off`.
  * Returns 0 when a frame was produced (crc_ok tells whether the CRC-16 matched; on a

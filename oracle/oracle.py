@@ -14,7 +14,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 SO = os.path.join(HERE, "build", "liboracle.so")
 
-EV_METADATA, EV_WRITE, EV_ERROR, EV_RETURN = 1, 2, 3, 4
+EV_METADATA, EV_WRITE, EV_ERROR, EV_RETURN, EV_SEEK = 1, 2, 3, 4, 5
 
 
 class Event(ctypes.Structure):
@@ -81,6 +81,26 @@ def run(data, driver=0, read_chunk=16384, write_abort_at=-1, max_events=None, ma
         raise RuntimeError(f"oracle_run rc={rc}")
     if npcm.value > max_pcm:
         return run(data, driver, read_chunk, write_abort_at, max_events, int(npcm.value))
+    return list(ev[: nev.value]), pcm[: npcm.value].copy()
+
+
+def run_seek(data, seeks, read_chunk=16384, max_events=None, max_pcm=None):
+    """FLACFileReader's seek pattern (seek_absolute from inside the write callback): seeks is a
+    list of (write_index | -1, target_sample); returns (events, pcm) like run()."""
+    b, n = _buf(data)
+    max_events = max_events or 4096 + n // 8
+    max_pcm = max_pcm or 1 << 22
+    ev = (Event * max_events)()
+    nev = ctypes.c_int()
+    pcm = np.zeros(max_pcm, dtype=np.int32)
+    npcm = ctypes.c_size_t()
+    arr = (ctypes.c_int64 * (2 * max(1, len(seeks))))(*[v for sk in seeks for v in sk])
+    rc = lib().oracle_run_seek(b, ctypes.c_size_t(n), read_chunk, arr, len(seeks), ev, max_events, ctypes.byref(nev),
+                               pcm.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(max_pcm), ctypes.byref(npcm))
+    if rc != 0:
+        raise RuntimeError(f"oracle_run_seek rc={rc}")
+    if npcm.value > max_pcm:
+        return run_seek(data, seeks, read_chunk, max_events, int(npcm.value))
     return list(ev[: nev.value]), pcm[: npcm.value].copy()
 
 

@@ -1,0 +1,103 @@
+"""Stream-API seeking on the GPU path against the oracle.
+
+The reference's only seek pattern is FLACFileReader's: setting Position makes the NEXT
+write callback copy its frame and then call FLAC__stream_decoder_seek_absolute from inside
+itself (FLACFileReader.cs:125-136, 267-301); the trimmed target frame arrives through a
+nested write callback and decoding continues after it.  harness.run(seeks=...) drives
+libbnflac.so that way and oracle.run_seek drives the CPU restatement the same way; the
+callback sequences (writes with blocksize and sample number, errors, metadata, every
+process_* and seek_absolute return) and the delivered PCM must be identical.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+GOLD_DIR = os.path.join(os.path.dirname(__file__), "golden")
+GOLD = json.load(open(os.path.join(GOLD_DIR, "golden.json")))
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from birdnest.audio_amd import harness
+    return harness
+
+
+def _stream(cfg, **kw):
+    from birdnest.audio_amd import synth
+    p = synth.config(cfg, **kw)
+    s = synth.encode(p)
+    return s.data.tobytes(), s
+
+
+def _compare(harness, data, seeks, read_chunk=16384):
+    import oracle
+    ev, pcm = harness.run(data, seeks=seeks, read_chunk=read_chunk)
+    oev, opcm = oracle.run_seek(data, seeks, read_chunk=read_chunk)
+    assert ev == harness.oracle_events_as_tuples(oev)
+    assert np.array_equal(pcm, opcm)
+    return ev, pcm
+
+
+CASES = [
+    ("C2", dict(nframes=24), [(3, 20000), (6, 4096 * 2)]),            # forward mid-frame, then backward to a frame start
+    ("C2", dict(nframes=24), [(0, 0), (1, 24 * 4096 - 1)]),            # to the first and to the last sample
+    ("C2", dict(nframes=24), [(-1, 50000)]),                           # right after the metadata pass
+    ("C2", dict(nframes=24), [(-2, 12345)]),                           # before the metadata pass: no STREAMINFO callback
+    ("C3", dict(nframes=12), [(2, 3 * 8192 + 17), (4, 100)]),          # 24-bit M/S + wasted bits
+    ("C4", dict(nframes=40), [(5, 60000), (7, 5), (9, 150000)]),       # variable blocksize, mixed subframes
+    ("C5", dict(nframes=6, last_blocksize=0), [(1, 4096 * 4 + 1000)]),  # 8 channels, LPC-32
+]
+
+
+@pytest.mark.parametrize("cfg,kw,seeks", CASES)
+def test_seek_from_write_callback_matches_oracle(gpu, cfg, kw, seeks):
+    data, s = _stream(cfg, **kw)
+    ev, pcm = _compare(gpu, data, seeks)
+    seek_ret = [e for e in ev if e[0] == gpu.EV_SEEK]
+    assert len(seek_ret) == len(seeks) and all(e[1] == 1 for e in seek_ret)
+    if seeks[0][0] == -2:
+        assert not [e for e in ev if e[0] == gpu.EV_METADATA]  # suppressed while seeking
+
+
+def test_seek_delivers_source_pcm(gpu):
+    """After a seek the trimmed frame and everything after it equal the source PCM."""
+    data, s = _stream("C2", nframes=20)
+    target = 7 * 4096 + 1234
+    ev, pcm = gpu.run(data, seeks=[(-1, target)])
+    writes = [e for e in ev if e[0] == gpu.EV_WRITE]
+    assert writes[0][8] == target and writes[0][3] == 4096 - 1234
+    out = []
+    off = 0
+    for e in writes:
+        bs, ch = e[3], e[5]
+        out.append(pcm[off: off + bs * ch].reshape(ch, bs).T)
+        off += bs * ch
+    assert np.array_equal(np.concatenate(out), s.pcm[target:])
+
+
+def test_seek_is_windowed_not_a_stream_walk(gpu):
+    """A seek to the end of a 10 MB stream reads a few windows, not the stream: the client's
+    seek callback positions the probes (interpolation over decoded windows)."""
+    data, s = _stream("C2", nframes=1024)
+    stats = {}
+    target = 1020 * 4096 + 7
+    ev, pcm = gpu.run(data, seeks=[(-1, target)], stats=stats)
+    writes = [e for e in ev if e[0] == gpu.EV_WRITE]
+    assert writes[0][8] == target
+    assert stats["read_total"] < len(data) // 3, stats
+    _compare(gpu, data, [(-1, target)])
+
+
+def test_seek_refusals(gpu):
+    """Past the end: false, no callbacks; no seek callback: false."""
+    data, s = _stream("C2", nframes=8)
+    ev, pcm = _compare(gpu, data, [(2, 8 * 4096)])
+    assert [e for e in ev if e[0] == gpu.EV_SEEK][0][1] == 0

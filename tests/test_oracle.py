@@ -147,3 +147,31 @@ def test_generator_md5_and_determinism():
     assert np.array_equal(a.data, b.data) and np.array_equal(a.pcm, b.pcm)
     assert bytes(a.data[26:42]) == synth.md5(a.pcm.astype("<i2").tobytes())
     assert bytes(a.data[26:42]) == hashlib.md5(a.pcm.astype("<i2").tobytes()).digest()
+
+
+def test_oracle_seek_from_write_callback_delivers_source_pcm():
+    """oracle_seek_absolute (libFLAC 1.2.1 seek_absolute semantics) in FLACFileReader's
+    pattern: the nested write delivers the target frame trimmed, decoding continues after
+    it, every sample equals the generator's source PCM; a target past the end is refused."""
+    import oracle
+    from birdnest.audio_amd import synth
+    s = synth.encode(synth.config("C4", nframes=30, seed=21))
+    data = s.data.tobytes()
+    n = s.pcm.shape[0]
+    for seeks in ([(2, n // 2 + 11)], [(-1, 77), (4, n - 1)], [(-2, 5000)]):
+        ev, pcm = oracle.run_seek(data, seeks)
+        kinds = [e.kind for e in ev]
+        assert kinds.count(oracle.EV_SEEK) == len(seeks)
+        assert all(e.status == 1 for e in ev if e.kind == oracle.EV_SEEK)
+        if seeks[0][0] == -2:
+            assert oracle.EV_METADATA not in kinds
+        # the writes after the last seek are the source PCM from its target on
+        last = max(i for i, e in enumerate(ev) if e.kind == oracle.EV_SEEK)
+        first_w = max(i for i, e in enumerate(ev[:last]) if e.kind == oracle.EV_WRITE)
+        tail = [e for e in ev[first_w:] if e.kind == oracle.EV_WRITE]
+        assert tail[0].sample_number == seeks[-1][1]
+        got = np.concatenate([pcm[e.pcm_offset: e.pcm_offset + e.blocksize * e.channels]
+                              .reshape(e.channels, e.blocksize).T for e in tail])
+        assert np.array_equal(got, s.pcm[seeks[-1][1]:])
+    ev, pcm = oracle.run_seek(data, [(1, n)])
+    assert [e.status for e in ev if e.kind == oracle.EV_SEEK] == [0]
