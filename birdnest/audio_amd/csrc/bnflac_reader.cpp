@@ -60,6 +60,44 @@ bool parse_metadata(const uint8_t *d, uint64_t n, bnflac_stream_params &sp, uint
     return have && p <= n;
 }
 
+/* A frame header at byte p that read_frame_header_ would accept (sync, codes, UTF-8
+ * number, CRC-8; FLAC format / LibFlac.dll@0x10011d70); its coded number in *num. */
+bool header_ok(const uint8_t *d, uint64_t n, uint64_t p, uint64_t *num, uint32_t *is_sample) {
+    if (p + 6 > n || d[p] != 0xFF || (d[p + 1] >> 1) != 0x7C) return false;
+    const uint32_t b2 = d[p + 2], b3 = d[p + 3];
+    if ((b2 >> 4) == 0 || (b2 & 15) == 15 || (b3 >> 4) >= 11 || ((b3 >> 1) & 7) == 3 || ((b3 >> 1) & 7) == 7 || (b3 & 1))
+        return false;
+    uint64_t q = p + 4, v = d[q];
+    int extra;
+    if (!(v & 0x80)) extra = 0;
+    else if ((v & 0xE0) == 0xC0) { extra = 1; v &= 0x1F; }
+    else if ((v & 0xF0) == 0xE0) { extra = 2; v &= 0x0F; }
+    else if ((v & 0xF8) == 0xF0) { extra = 3; v &= 0x07; }
+    else if ((v & 0xFC) == 0xF8) { extra = 4; v &= 0x03; }
+    else if ((v & 0xFE) == 0xFC) { extra = 5; v &= 0x01; }
+    else if (v == 0xFE) { extra = 6; v = 0; }
+    else return false;
+    q++;
+    for (int i = 0; i < extra; i++, q++) {
+        if (q >= n || (d[q] & 0xC0) != 0x80) return false;
+        v = (v << 6) | (d[q] & 0x3F);
+    }
+    if ((b2 >> 4) == 6) q += 1;
+    else if ((b2 >> 4) == 7) q += 2;
+    if ((b2 & 15) == 12) q += 1;
+    else if ((b2 & 15) == 13 || (b2 & 15) == 14) q += 2;
+    if (q >= n) return false;
+    uint8_t c = 0; /* CRC-8, poly 0x07 */
+    for (uint64_t i = p; i < q; i++) {
+        c ^= d[i];
+        for (int b = 0; b < 8; b++) c = (uint8_t)((c & 0x80) ? (c << 1) ^ 0x07 : (c << 1));
+    }
+    if (c != d[q]) return false;
+    *num = v;
+    *is_sample = d[p + 1] & 1;
+    return true;
+}
+
 } // namespace
 
 struct bnflac_reader {
@@ -85,6 +123,14 @@ struct bnflac_reader {
     uint64_t total_bytes = 0, returned = 0;
     std::vector<bnflac_frame_info> winfo;
     bool failed = false;
+    /* FLACFileReader compat mode (bnflac_reader_read_filereader): the C# reader's state */
+    int mode = 0;                 /* 0 unused, 1 byte reads (bnflac_reader_read), 2 FLACFileReader reads */
+    uint32_t fr_next = 0;         /* next frame "ProcessSingle" decodes */
+    bool fr_landed = false;       /* window r->cur has landed (compat mode) */
+    uint32_t spc = 0;             /* m_samplesPerChannel: the first frame's blocksize */
+    uint32_t fr_idx = 0;          /* m_flacSampleIndex */
+    std::vector<uint8_t> image;   /* m_flacSamples, packed: spc sample frames x channels x bytes */
+    bool eos = false;             /* decoder state reached EndOfStream */
 };
 
 namespace {
@@ -232,6 +278,33 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
         return rfail("bnflac_reader_open: the frame chain covers " + std::to_string(end) + " of " +
                      std::to_string(r->sp.total_samples) + " samples (damaged stream: use the libFLAC stream API)");
     }
+    if (!r->sp.total_samples && nf) {
+        /* length unknown (STREAMINFO total 0): a damaged frame would end the chain early with
+         * every chained frame intact.  Refuse when an acceptable header numbered past the
+         * chain's last frame follows it (trailing tags and metadata are allowed). */
+        uint64_t last_off = 0;
+        bnflac_frame_info last;
+        if (hipMemcpy(&last_off, (uint64_t *)r->d_offs + (nf - 1), 8, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(&last, (bnflac_frame_info *)r->d_info + (nf - 1), sizeof last, hipMemcpyDeviceToHost) != hipSuccess) {
+            release(r);
+            return rfail("bnflac_reader_open: D2H copy failed");
+        }
+        const uint64_t last_no = last.number_type ? r->os[nf - 1] : last.number;
+        for (uint64_t p = last_off + 2; p + 1 < nbytes; p++) {
+            uint64_t no = 0;
+            uint32_t is_sample = 0;
+            if (bytes[p] != 0xFF || !header_ok(bytes, nbytes, p, &no, &is_sample)) continue;
+            const uint64_t room = (nbytes - p) / 16 + 1; /* frames that could still follow */
+            const bool plausible = is_sample ? (no >= end && no <= end + room * 65536ull)
+                                             : (no > last_no && no <= last_no + 1 + room);
+            if (plausible) {
+                release(r);
+                return rfail("bnflac_reader_open: the frame chain ends at byte " + std::to_string(last_off) +
+                             " but a frame header follows at byte " + std::to_string(p) +
+                             " (damaged stream: use the libFLAC stream API)");
+            }
+        }
+    }
     r->total_bytes = end * r->stride;
     r->nwin = (nf + r->window - 1) / r->window;
     for (uint32_t w = 0; w < r->nwin; w++) r->slot_bytes = std::max<size_t>(r->slot_bytes, win_bytes(r, w));
@@ -265,6 +338,8 @@ BNFLAC_API int bnflac_reader_params(const bnflac_reader *r, bnflac_stream_params
 BNFLAC_API int64_t bnflac_reader_read(bnflac_reader *r, uint8_t *buf, uint64_t count) {
     if (!r) return rfail("bnflac_reader_read: null reader");
     if (r->failed) return rfail("bnflac_reader_read: reader failed earlier");
+    if (r->mode == 2) return rfail("bnflac_reader_read: this reader is in FLACFileReader mode");
+    r->mode = 1;
     if (!buf && count) return rfail("bnflac_reader_read: null buffer");
     uint64_t done = 0;
     while (done < count && r->cur < r->nwin) {
@@ -290,12 +365,70 @@ BNFLAC_API int64_t bnflac_reader_read(bnflac_reader *r, uint8_t *buf, uint64_t c
     return (int64_t)done;
 }
 
+/* ---- FLACFileReader compat mode: FLACFileReader.Read(buffer, offset, numBytes) replayed over
+ * the decoded frames (FLACFileReader.cs:145-174, 208-254, 267-301). */
+
+/* ProcessSingle: the next frame's packed bytes (FILEREADER layout, bs sample frames) */
+int fr_next_frame(bnflac_reader *r, const uint8_t **bytes, uint32_t *bs) {
+    if (r->fr_next >= r->nframes) return 0;
+    const uint32_t f = r->fr_next, w = f / r->window;
+    while (r->cur < w) { /* the window before is done: its slot takes the window after the next */
+        if (issue_window(r, r->cur + 2)) return -1;
+        r->cur++;
+        r->fr_landed = false;
+    }
+    if (!r->fr_landed) {
+        if (land_window(r, w)) return -1;
+        r->fr_landed = true;
+    }
+    const uint64_t f0 = (uint64_t)w * r->window;
+    *bytes = r->ring[w & 1u] + (r->os[f] - r->os[f0]) * r->stride;
+    *bs = (uint32_t)(r->os[f + 1] - r->os[f]);
+    r->fr_next++;
+    return 1;
+}
+
+/* FLAC_WriteCallback: the first frame fixes m_samplesPerChannel; every frame overwrites the
+ * first min(bs, spc) samples of m_flacSamples (libFLAC's buffers keep the rest: a short
+ * frame leaves the previous frames' samples behind, a long one is truncated) */
+void fr_write(bnflac_reader *r, const uint8_t *bytes, uint32_t bs) {
+    const uint32_t sf = r->stride; /* bytes per sample frame: channels x (2 | 3) */
+    if (!r->spc) {
+        r->spc = bs;
+        r->image.assign((size_t)bs * sf, 0);
+        r->fr_idx = 0;
+    }
+    memcpy(r->image.data(), bytes, (size_t)std::min(bs, r->spc) * sf);
+}
+
+/* CopyFlacBufferToNAudioBuffer: sample-major, channel-minor, until the buffer's LENGTH
+ * (not offset + numBytes); returns bytes copied or -1 (IndexOutOfRange: a sample that does
+ * not fit, after its leading bytes were written, as the C# byte loop does) */
+int64_t fr_copy(bnflac_reader *r, uint8_t *buf, uint64_t len, uint64_t &noff) {
+    const uint64_t start = noff;
+    const uint32_t C = r->sp.channels, fb = r->sp.bps == 24 ? 3u : 2u;
+    bool full = noff >= len;
+    for (; r->fr_idx < r->spc && !full; r->fr_idx++) {
+        for (uint32_t ch = 0; ch < C && !full; ch++) {
+            const uint8_t *smp = r->image.data() + ((size_t)r->fr_idx * C + ch) * fb;
+            for (uint32_t k = 0; k < fb; k++) {
+                if (noff >= len) return -1;
+                buf[noff++] = smp[k];
+            }
+            full = noff >= len;
+        }
+    }
+    if (r->fr_idx >= r->spc) r->fr_idx = 0;
+    return (int64_t)(noff - start);
+}
+
 /* FLACFileReader.Position / seek_absolute (FLACFileReader.cs:109-137,295-299): the next read
  * starts at sample `sample` (per channel).  The frame holding it is found in the index
  * (binary search over the running sample counts); its window and the next are decoded
  * again and the reader resumes inside the first. */
 BNFLAC_API int bnflac_reader_seek(bnflac_reader *r, uint64_t sample) {
     if (!r) return rfail("bnflac_reader_seek: null reader");
+    if (r->mode == 2) return rfail("bnflac_reader_seek: not available in FLACFileReader mode");
     if (r->failed) return rfail("bnflac_reader_seek: reader failed earlier");
     const uint64_t total = r->os[r->nframes];
     if (sample >= total) return rfail("bnflac_reader_seek: sample past the end of the stream");
@@ -316,6 +449,58 @@ BNFLAC_API int bnflac_reader_seek(bnflac_reader *r, uint64_t sample) {
     r->cur_pos = (sample - r->os[(size_t)w * r->window]) * r->stride;
     r->returned = sample * r->stride;
     return 0;
+}
+
+/* FLACFileReader.Read(buffer, offset, numBytes) with buffer.Length = buffer_length
+ * (FLACFileReader.cs:145-174): drain the carried-over samples, then "ProcessSingle" +
+ * copy until numBytes are reached or the stream ends; the copy runs to the end of the
+ * buffer, so the return may exceed numBytes.  Exceptions of the C# surface return -1 with
+ * their message (bnflac_reader_last_error): IndexOutOfRange for a sample that does not fit
+ * the buffer, NotSupported for bit depths other than 16 and 24.  Needs a reader opened with
+ * the FILEREADER layout; byte reads and seeks are not mixed with it. */
+BNFLAC_API int64_t bnflac_reader_read_filereader(bnflac_reader *r, uint8_t *buffer, uint64_t offset, uint64_t num_bytes,
+                                                 uint64_t buffer_length) {
+    if (!r) return rfail("bnflac_reader_read_filereader: null reader");
+    if (r->failed) return rfail("bnflac_reader_read_filereader: reader failed earlier");
+    if (r->fmt != BNFLAC_OUT_FILEREADER) return rfail("bnflac_reader_read_filereader: reader not opened with the FILEREADER layout");
+    if (r->mode == 1) return rfail("bnflac_reader_read_filereader: this reader already serves byte reads");
+    if (!buffer && buffer_length) return rfail("bnflac_reader_read_filereader: null buffer");
+    r->mode = 2;
+    uint64_t noff = offset;
+    int64_t copied = 0;
+    if (r->fr_idx > 0) {
+        if (r->sp.bps != 16 && r->sp.bps != 24) return rfail("Input FLAC bit depth is not supported!");
+        const int64_t c = fr_copy(r, buffer, buffer_length, noff);
+        if (c < 0) return rfail("Index was outside the bounds of the array.");
+        copied = c;
+    }
+    while ((uint64_t)copied < num_bytes) {
+        if (r->eos) break;
+        if (r->sp.bps != 16 && r->sp.bps != 24) { /* the first frame decodes, its copy throws */
+            if (r->fr_next >= r->nframes) {
+                r->eos = true;
+                break;
+            }
+            r->fr_next++;
+            return rfail("Input FLAC bit depth is not supported!");
+        }
+        const uint8_t *fb = nullptr;
+        uint32_t bs = 0;
+        const int g = fr_next_frame(r, &fb, &bs);
+        if (g < 0) {
+            r->failed = true;
+            return -1;
+        }
+        if (g == 0) { /* the decoder reached EndOfStream */
+            r->eos = true;
+            break;
+        }
+        fr_write(r, fb, bs);
+        const int64_t c = fr_copy(r, buffer, buffer_length, noff);
+        if (c < 0) return rfail("Index was outside the bounds of the array.");
+        copied += c;
+    }
+    return copied;
 }
 
 BNFLAC_API void bnflac_reader_close(bnflac_reader *r) {

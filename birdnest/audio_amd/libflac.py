@@ -127,7 +127,7 @@ BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error",
                  "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats", "bnflac_debug_set_crc_pass",
                  "bnflac_md5_interleaved32", "bnflac_index_stream"]
 READER_SYMBOLS = ["bnflac_reader_open", "bnflac_reader_params", "bnflac_reader_read", "bnflac_reader_close",
-                  "bnflac_reader_last_error", "bnflac_reader_seek"]
+                  "bnflac_reader_last_error", "bnflac_reader_seek", "bnflac_reader_read_filereader"]
 
 _LIB = None
 
@@ -191,6 +191,8 @@ def load() -> ctypes.CDLL:
     L.bnflac_reader_read.restype = ctypes.c_int64
     L.bnflac_reader_read.argtypes = [p, p, ctypes.c_uint64]
     L.bnflac_reader_close.argtypes = [p]
+    L.bnflac_reader_read_filereader.restype = ctypes.c_int64
+    L.bnflac_reader_read_filereader.argtypes = [p, p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
     L.bnflac_reader_seek.restype = i
     L.bnflac_reader_seek.argtypes = [p, ctypes.c_uint64]
     L.bnflac_reader_last_error.restype = ctypes.c_char_p
@@ -432,6 +434,33 @@ class Reader:
         if n < 0:
             raise RuntimeError(self.L.bnflac_reader_last_error().decode())
         return int(n)
+
+    def ReadFileReader(self, buffer: bytearray, offset: int, count: int) -> int:
+        """FLACFileReader.Read(buffer, offset, numBytes) semantics (bnflac_reader_read_filereader):
+        copies may run past offset + count up to len(buffer); C# exceptions raise RuntimeError."""
+        if offset < 0 or count < 0:
+            raise ValueError("negative offset/count")
+        view = (ctypes.c_uint8 * len(buffer)).from_buffer(buffer) if len(buffer) else None
+        n = self.L.bnflac_reader_read_filereader(self.h, ctypes.addressof(view) if view is not None else None, offset,
+                                                 count, len(buffer))
+        if n < 0:
+            raise RuntimeError(self.L.bnflac_reader_last_error().decode())
+        return int(n)
+
+    def filereader_read_all(self, buf_len: int, num_bytes: int = None):
+        """Read(buf, 0, num_bytes) on a buf_len-byte buffer until 0, like
+        oracle.filereader_readall -> (rc, bytes, message)."""
+        num_bytes = buf_len if num_bytes is None else num_bytes
+        out = bytearray()
+        buf = bytearray(buf_len)
+        try:
+            while True:
+                n = self.ReadFileReader(buf, 0, num_bytes)
+                if n == 0:
+                    return 0, bytes(out), ""
+                out += buf[:n]
+        except RuntimeError as e:
+            return 1, bytes(out), str(e)
 
     def Seek(self, sample: int):
         """Next Read starts at this sample (per channel): FLACFileReader.Position."""

@@ -218,6 +218,16 @@ BNFLAC_API int64_t bnflac_reader_read(bnflac_reader *reader, uint8_t *buf, uint6
  * FLACFileReader.Position / seek_absolute (FLACFileReader.cs:109-137,295-299).  0 or -1
  * (sample past the end, or damage in the target window). */
 BNFLAC_API int bnflac_reader_seek(bnflac_reader *reader, uint64_t sample);
+/* FLACFileReader.Read(buffer, offset, numBytes) (FLACFileReader.cs:145-254) replayed with
+ * buffer.Length = buffer_length, on a reader opened with BNFLAC_OUT_FILEREADER: samples left
+ * over from the previous call first, then whole frames until numBytes are reached; every copy
+ * runs to the buffer's end (the return may exceed num_bytes), m_samplesPerChannel is the first
+ * frame's blocksize (shorter frames leave earlier samples behind, longer ones are cut).
+ * Returns the bytes copied, 0 at the end, -1 with the C# exception's message in
+ * bnflac_reader_last_error() ("Index was outside the bounds of the array." / "Input FLAC bit
+ * depth is not supported!").  Not mixed with bnflac_reader_read / bnflac_reader_seek. */
+BNFLAC_API int64_t bnflac_reader_read_filereader(bnflac_reader *reader, uint8_t *buffer, uint64_t offset,
+                                                 uint64_t num_bytes, uint64_t buffer_length);
 BNFLAC_API void bnflac_reader_close(bnflac_reader *reader);
 BNFLAC_API const char *bnflac_reader_last_error(void);
 

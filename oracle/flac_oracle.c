@@ -1768,6 +1768,13 @@ static int cfr_copy(cfr_client *c) {
 
 int oracle_filereader_readall(const uint8_t *data, size_t len, int buf_len, uint8_t *out,
                               size_t cap, size_t *out_len, char *msg, int msg_cap) {
+    return oracle_filereader_readall_n(data, len, buf_len, buf_len, out, cap, out_len, msg, msg_cap);
+}
+
+/* The same with Read(buf, 0, num_bytes) on a buffer of buf_len bytes: the copy loop runs to
+ * buf.Length, so a call may return more than num_bytes (FLACFileReader.cs:162-171, 211). */
+int oracle_filereader_readall_n(const uint8_t *data, size_t len, int buf_len, int num_bytes, uint8_t *out,
+                                size_t cap, size_t *out_len, char *msg, int msg_cap) {
     cfr_client *c = (cfr_client *)calloc(1, sizeof(cfr_client));
     c->mc.data = data; c->mc.len = len; c->mc.chunk = 1 << 30; /* init_file reads with fread */
     c->msg = msg; c->msg_cap = msg_cap;
@@ -1798,7 +1805,7 @@ int oracle_filereader_readall(const uint8_t *data, size_t len, int buf_len, uint
                 copied = r;
             }
             int spins = 0;
-            while (copied < buf_len) {
+            while (copied < num_bytes) {
                 if (++spins > 10000000) { /* the C# loop never ends (e.g. state Aborted) */
                     snprintf(msg, (size_t)msg_cap, "hang: Read() never returns (state %s)",
                              state_name((int)d->state));

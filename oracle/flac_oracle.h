@@ -122,6 +122,9 @@ int oracle_flacdecoder_copyto(const uint8_t *data, size_t len, int copy_chunk, u
  * (FLACFileReader.cs:45-78, 145-254, 267-329). */
 int oracle_filereader_readall(const uint8_t *data, size_t len, int buf_len, uint8_t *out,
                               size_t cap, size_t *out_len, char *msg, int msg_cap);
+/* ... with Read(buf, 0, num_bytes) on a buf_len-byte buffer (num_bytes <= buf_len: overfill) */
+int oracle_filereader_readall_n(const uint8_t *data, size_t len, int buf_len, int num_bytes, uint8_t *out,
+                                size_t cap, size_t *out_len, char *msg, int msg_cap);
 
 /* CRC helpers (poly 0x07 / 0x8005, init 0) -- exported for the generator tests. */
 uint8_t oracle_crc8(const uint8_t *p, size_t n);

@@ -141,14 +141,17 @@ def flacdecoder_copyto(data, copy_chunk=81920):
     return rc, out[: olen.value].tobytes(), msg.value.decode(), list(fmt)
 
 
-def filereader_readall(data, buf_len=4096 * 6):
+def filereader_readall(data, buf_len=4096 * 6, num_bytes=None):
+    """FLACFileReader ctor + Read(buf, 0, num_bytes) on a buf_len-byte buffer until it returns
+    0 (num_bytes defaults to buf_len).  -> (rc, bytes of every returned read, message)."""
     b, n = _buf(data)
     cap = n * 8 + (1 << 20)
     out = np.zeros(cap, dtype=np.uint8)
     olen = ctypes.c_size_t()
     msg = ctypes.create_string_buffer(512)
-    rc = lib().oracle_filereader_readall(b, ctypes.c_size_t(n), buf_len, out.ctypes.data_as(ctypes.c_void_p),
-                                         ctypes.c_size_t(cap), ctypes.byref(olen), msg, 512)
+    rc = lib().oracle_filereader_readall_n(b, ctypes.c_size_t(n), buf_len, buf_len if num_bytes is None else num_bytes,
+                                           out.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(cap),
+                                           ctypes.byref(olen), msg, 512)
     return rc, out[: olen.value].tobytes(), msg.value.decode()
 
 

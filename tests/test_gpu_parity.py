@@ -572,13 +572,54 @@ def test_reader_matches_flacdecoder_copyto(gpu, name):
     data = _read(name)
     rc, pk, msg, fmt = flac_decoder.copy_to_bytes(data)
     if rc != 0 or fmt[2] != 16:
-        pytest.skip(f"FLACDecoder does not yield this stream: {msg or fmt}")
+        # FLACDecoder aborts on these (FLACDecoder.cs:526-530); FLACFileReader is the
+        # reference's reader for them: its Read semantics against the oracle's replay
+        _filereader_vs_oracle(libflac, data)
+        return
     r = libflac.Reader(data, libflac.OUT_FLACDECODER, window_frames=5)
     try:
         assert r.total_bytes == len(pk)
         assert r.read_all(16384) == pk
     finally:
         r.close()
+
+
+def _filereader_vs_oracle(libflac, data, windows=(3,)):
+    """bnflac_reader in FLACFileReader mode == oracle.filereader_readall, byte for byte and
+    exception for exception, over buffer lengths that hit the reader's quirks: one frame,
+    half a frame (carry-over between calls), a length that is not a whole number of samples
+    (IndexOutOfRange), and Read(buf, 0, n) with n far below buf.Length (overfill)."""
+    import oracle
+    si = data[8:42]
+    x = int.from_bytes(si[10:18], "big")
+    ch, bps = ((x >> 41) & 7) + 1, ((x >> 36) & 31) + 1
+    maxbs = int.from_bytes(si[2:4], "big")
+    sf = ch * (3 if bps == 24 else 2)
+    cases = [(maxbs * sf, None), (maxbs * sf // 2 + sf, None), (sf * 100 + 1, None), (maxbs * sf * 3, 7),
+             (sf * 37, None)]
+    for win in windows:
+        for buf_len, nb in cases:
+            rc, ref, msg = oracle.filereader_readall(data, buf_len, nb)
+            r = libflac.Reader(data, libflac.OUT_FILEREADER, window_frames=win)
+            try:
+                grc, got, gmsg = r.filereader_read_all(buf_len, nb)
+            finally:
+                r.close()
+            assert (grc, gmsg) == (rc, msg), (buf_len, nb)
+            assert got == ref, (buf_len, nb, len(got), len(ref))
+
+
+def test_filereader_mode_quirks_24bit(gpu):
+    """FLACFileReader surface on the 24-bit configs (its only reference path, FLACFileReader.cs:
+    230-237): a short last frame (stale tail: m_samplesPerChannel fixed by the first frame),
+    variable blocksizes (truncation), carry-over, overfill and IndexOutOfRange, all against
+    the oracle's replay."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    for cfg, kw in (("C3", dict(nframes=5, last_blocksize=3000)), ("C5", dict(nframes=4, last_blocksize=1500)),
+                    ("C4", dict(nframes=30, bps=24, seed=7)), ("C1", dict(nframes=6, last_blocksize=100))):
+        s = synth.encode(synth.config(cfg, **kw))
+        _filereader_vs_oracle(libflac, s.data.tobytes(), windows=(2, 64))
 
 
 @pytest.mark.parametrize("window,chunk", [(256, 16384), (7, 1000), (1, 4096 * 4 + 3)])
@@ -615,6 +656,33 @@ def test_reader_refuses_damaged_stream(gpu):
         libflac.Reader(b"not a flac stream at all", libflac.OUT_FLACDECODER)
     with pytest.raises(RuntimeError, match="16-bit"):
         libflac.Reader(_read("c3_lpc12_ms_wasted"), libflac.OUT_FLACDECODER)
+
+
+def _zero_total(data: bytes) -> bytearray:
+    """STREAMINFO total_samples := 0 (unknown length): the low 36 bits of bytes 21..25."""
+    d = bytearray(data)
+    d[21] &= 0xF0
+    d[22:26] = bytes(4)
+    return d
+
+
+def test_reader_unknown_length_refuses_a_cut_chain(gpu):
+    """total_samples 0: a damaged mid-stream header ends the GPU frame chain early with every
+    chained frame intact -- the reader must refuse, not return a prefix; an
+    intact stream with trailing non-frame bytes (an ID3v1 tag) still reads completely."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    s = synth.encode(synth.config("C2", nframes=12))
+    d = _zero_total(s.data.tobytes())
+    r = libflac.Reader(bytes(d) + b"TAG" + bytes(125), libflac.OUT_FLACDECODER, window_frames=4)
+    try:
+        assert r.read_all(16384) == s.pcm.astype("<i2").tobytes()
+    finally:
+        r.close()
+    o = [int(x) for x in s.frame_offsets]
+    d[o[5] + 4] ^= 0x55  # frame 5's header (its CRC-8 no longer matches)
+    with pytest.raises(RuntimeError, match="damaged"):
+        libflac.Reader(bytes(d), libflac.OUT_FLACDECODER, window_frames=4).close()
 
 
 def test_reader_seek(gpu):
