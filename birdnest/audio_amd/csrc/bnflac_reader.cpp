@@ -27,6 +27,19 @@
 namespace {
 
 thread_local std::string g_rerr;
+
+/* run on the reader's device, restore the caller's on scope exit */
+struct RDevGuard {
+    int prev = -1;
+    explicit RDevGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~RDevGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
 int rfail(const std::string &m) {
     g_rerr = m;
     return -1;
@@ -203,6 +216,8 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
     *out = nullptr;
     if (!bytes) return rfail("bnflac_reader_open: null bytes");
     if (out_format < 0 || out_format > 3) return rfail("bnflac_reader_open: bad out_format");
+    if (device < 0 || device >= bnflac_device_count()) return rfail("bnflac_reader_open: bad device index");
+    RDevGuard dg(device);
     bnflac_reader *r = new bnflac_reader();
     r->device = device;
     r->fmt = out_format;
@@ -337,6 +352,7 @@ BNFLAC_API int bnflac_reader_params(const bnflac_reader *r, bnflac_stream_params
 
 BNFLAC_API int64_t bnflac_reader_read(bnflac_reader *r, uint8_t *buf, uint64_t count) {
     if (!r) return rfail("bnflac_reader_read: null reader");
+    RDevGuard dg(r->device);
     if (r->failed) return rfail("bnflac_reader_read: reader failed earlier");
     if (r->mode == 2) return rfail("bnflac_reader_read: this reader is in FLACFileReader mode");
     r->mode = 1;
@@ -428,6 +444,7 @@ int64_t fr_copy(bnflac_reader *r, uint8_t *buf, uint64_t len, uint64_t &noff) {
  * again and the reader resumes inside the first. */
 BNFLAC_API int bnflac_reader_seek(bnflac_reader *r, uint64_t sample) {
     if (!r) return rfail("bnflac_reader_seek: null reader");
+    RDevGuard dg(r->device);
     if (r->mode == 2) return rfail("bnflac_reader_seek: not available in FLACFileReader mode");
     if (r->failed) return rfail("bnflac_reader_seek: reader failed earlier");
     const uint64_t total = r->os[r->nframes];
@@ -461,6 +478,7 @@ BNFLAC_API int bnflac_reader_seek(bnflac_reader *r, uint64_t sample) {
 BNFLAC_API int64_t bnflac_reader_read_filereader(bnflac_reader *r, uint8_t *buffer, uint64_t offset, uint64_t num_bytes,
                                                  uint64_t buffer_length) {
     if (!r) return rfail("bnflac_reader_read_filereader: null reader");
+    RDevGuard dg(r->device);
     if (r->failed) return rfail("bnflac_reader_read_filereader: reader failed earlier");
     if (r->fmt != BNFLAC_OUT_FILEREADER) return rfail("bnflac_reader_read_filereader: reader not opened with the FILEREADER layout");
     if (r->mode == 1) return rfail("bnflac_reader_read_filereader: this reader already serves byte reads");
@@ -504,7 +522,9 @@ BNFLAC_API int64_t bnflac_reader_read_filereader(bnflac_reader *r, uint8_t *buff
 }
 
 BNFLAC_API void bnflac_reader_close(bnflac_reader *r) {
-    if (r) release(r);
+    if (!r) return;
+    RDevGuard dg(r->device);
+    release(r);
 }
 
 } /* extern "C" */

@@ -94,6 +94,20 @@ static void build_tables(uint8_t *c8, uint16_t *c16, uint16_t *xp) {
     }
 }
 
+/* The caller's current HIP device is restored on scope exit (the library never leaves the
+ * thread on another device). */
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DevGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
 static std::mutex g_dev_mu;
 static bool g_tables_ready[64];
 
@@ -102,7 +116,7 @@ static int ensure_device(int dev) {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail("bnflac: no HIP device available (the decode path is GPU-only)");
     if (dev < 0 || dev >= n || dev >= 64) return fail("bnflac: bad device index");
     std::lock_guard<std::mutex> lk(g_dev_mu);
-    if (hipSetDevice(dev) != hipSuccess) return fail("bnflac: hipSetDevice failed");
+    DevGuard g(dev);
     if (!g_tables_ready[dev]) {
         uint8_t c8[256];
         uint16_t c16[8 * 256], xp[40];
@@ -217,6 +231,7 @@ extern "C" BNFLAC_API int bnflac_md5_interleaved32(const int32_t *pcm, uint64_t 
 extern "C" BNFLAC_API int bnflac_index_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
                                               uint64_t *d_offsets, uint32_t cap, uint32_t *d_count, void *hs) {
     if (!ctx) return fail("bnflac_index_frames: null ctx");
+    DevGuard dg(ctx->device); /* launches and scratch on the context's device */
     if (((uintptr_t)d_bytes) & 3u) return fail("bnflac_index_frames: d_bytes must be 4-byte aligned");
     const uint32_t nb = bnf_scan_blocks(nbytes);
     if (nb > ctx->block_cap) {
@@ -244,6 +259,7 @@ extern "C" BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_
                                               const bnflac_stream_params *sp, const uint64_t *d_out_sample,
                                               uint64_t base_sample, bnflac_frame_info *d_info, void *hs) {
     if (check_args(ctx, d_bytes, nbytes, sp, "bnflac_parse_frames")) return -1;
+    DevGuard dg(ctx->device); /* launches and scratch on the context's device */
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, d_frame_offsets,
@@ -256,6 +272,7 @@ extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d
                                                const bnflac_stream_params *sp, int out_format, uint8_t *d_out,
                                                uint64_t out_bytes, bnflac_frame_info *d_info, void *hs) {
     if (check_args(ctx, d_bytes, nbytes, sp, "bnflac_decode_parsed")) return -1;
+    DevGuard dg(ctx->device); /* launches and scratch on the context's device */
     if (out_format < 0 || out_format > 3) return fail("bnflac_decode_parsed: bad out_format");
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
@@ -281,6 +298,7 @@ extern "C" BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_
                                               uint64_t *d_frame_offsets, uint64_t *d_out_sample,
                                               bnflac_frame_info *d_info, uint32_t cap, uint32_t *d_nframes, void *hs) {
     if (check_args(ctx, d_bytes, nbytes, sp, "bnflac_index_stream")) return -1;
+    DevGuard dg(ctx->device); /* launches and scratch on the context's device */
     if (!d_frame_offsets || !d_nframes) return fail("bnflac_index_stream: null output");
     hipStream_t s = (hipStream_t)hs;
     /* 1. sync candidates (one host sync for their count) */
@@ -417,19 +435,6 @@ using Dec = FLAC__StreamDecoder;
 uint64_t bend(const Dec *d) { return d->buf_base + d->buf.size(); } /* one past the last buffered byte */
 uint8_t bat(const Dec *d, uint64_t p) { return d->buf[(size_t)(p - d->buf_base)]; }
 
-/* The caller's current HIP device is restored on scope exit (the library never leaves the
- * thread on another device). */
-struct DevGuard {
-    int prev = -1;
-    explicit DevGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DevGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
 
 /* read_callback_ (stream_decoder.c) semantics, without touching the decoder state:
  * 0 = got bytes, 1 = end of stream, 2 = abort. */
@@ -808,7 +813,10 @@ const bnf_frame_info *lookup(Dec *d, uint64_t p) {
 void allocate_output(Dec *d, unsigned size, unsigned ch) {
     if (size <= d->output_capacity && ch <= d->output_channels) return;
     for (unsigned i = 0; i < FLAC__MAX_CHANNELS; i++) d->output[i].clear();
-    for (unsigned i = 0; i < ch; i++) d->output[i].assign(size ? size : 1, 0);
+    /* twice the capacity: a client that copies more than the frame (FLACFileReader copies
+     * the first frame's blocksize from a trimmed seek frame, FLACFileReader.cs:287) reads
+     * stale values instead of running off the allocation */
+    for (unsigned i = 0; i < ch; i++) d->output[i].assign(2u * (size ? size : 1), 0);
     d->output_capacity = size;
     d->output_channels = ch;
 }
