@@ -872,6 +872,34 @@ DEV int32_t next_val(BR &b, RS &s, uint64_t limit, uint32_t &trunc) {
     return rice_one(b, s.k, limit, trunc);
 }
 
+/* next residual on the fused paths: a new partition's header and escaped (raw) partitions
+ * inline behind wave-uniform tests, so a chunk need not lie inside one partition; Rice
+ * codewords as rice_one.  An escaped lane issues its pending row write itself. */
+DEV int32_t rice_fused(BR &b, RS &rs, uint64_t limit, uint32_t &trunc, PendW *pw) {
+    const bool np = rs.left == 0;
+    if (__builtin_expect(any_lane(np), 0)) {
+        if (np) {
+            do { /* partition 0 holds no samples when the order equals the partition size */
+                if (rs.pidx < rs.nparts) {
+                    read_partition(b, rs);
+                } else { /* more samples than the partitions carry: a damaged frame */
+                    trunc = 1;
+                    rs.left = 0x7fffffffu;
+                }
+            } while (rs.left == 0);
+        }
+    }
+    rs.left--;
+    if (__builtin_expect(any_lane(rs.esc != 0u), 0)) {
+        if (rs.esc) {
+            if (pw && pw->on) *pw->at = pw->v;
+            if (pw) pw->on = false;
+            return br_read_s(b, rs.k);
+        }
+    }
+    return rice_one(b, rs.k, limit, trunc, pw);
+}
+
 DEV void finish_partitions(BR &b, RS &s) {
     if (s.verb) return;
     while (s.pidx < s.nparts) {
@@ -975,21 +1003,21 @@ DEV void lpc_chunk(int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t
 /* samples T..W-1 of one W-sample group, unrolled by recursion so every history index is a
  * compile-time constant (a rolled loop puts the ring behind s_set_gpr_idx moves) */
 template <int T, int W, int P, int N>
-DEV void lpc_fused_steps(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
+DEV void lpc_fused_steps(BR &b, RS &rs, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
                          int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc, PendW &pw, int j) {
     if constexpr (T < W) {
-        const int32_t r = rice_one(b, k, limit, trunc, &pw);
+        const int32_t r = rice_fused(b, rs, limit, trunc, &pw);
         const int32_t s = (int32_t)((uint32_t)r + (uint32_t)lpc_pred<W, P>(c, h, ht, T, sh));
         lpc_push<W, P>(h, ht, T, s);
         pw.v = (int32_t)((uint32_t)s << wasted);
         pw.at = row + (j + T) * RP;
         pw.on = true;
-        lpc_fused_steps<T + 1, W, P, N>(b, k, row, c, h, ht, sh, wasted, limit, trunc, pw, j);
+        lpc_fused_steps<T + 1, W, P, N>(b, rs, row, c, h, ht, sh, wasted, limit, trunc, pw, j);
     }
 }
 
 template <int CH, int W, int P, int N>
-DEV void lpc_fused(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
+DEV void lpc_fused(BR &b, RS &rs, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
                    int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc) {
     /* each sample's row write is issued just before the next codeword's ring read, so the
      * next LDS wait (hipcc waits lgkmcnt(0) here) finds every LDS op a codeword old */
@@ -998,7 +1026,7 @@ DEV void lpc_fused(BR &b, uint32_t k, int32_t *row, const int32_t (&c)[N], int32
     pw.v = 0;
     pw.on = false;
 #pragma unroll 1
-    for (int j = 0; j < CH; j += W) lpc_fused_steps<0, W, P, N>(b, k, row, c, h, ht, sh, wasted, limit, trunc, pw, j);
+    for (int j = 0; j < CH; j += W) lpc_fused_steps<0, W, P, N>(b, rs, row, c, h, ht, sh, wasted, limit, trunc, pw, j);
     *pw.at = pw.v;
 }
 
@@ -1032,7 +1060,7 @@ DEV void fixed_chunk(int32_t *row, int32_t (&h)[N], uint32_t n0, uint32_t nvalid
 }
 
 template <int CH, int N>
-DEV void fixed_fused(BR &b, uint32_t k, int32_t *row, int32_t (&h)[N], uint32_t order, uint32_t wasted,
+DEV void fixed_fused(BR &b, RS &rs, int32_t *row, int32_t (&h)[N], uint32_t order, uint32_t wasted,
                      uint64_t limit, uint32_t &trunc) {
     PendW pw;
     pw.at = row;
@@ -1042,7 +1070,7 @@ DEV void fixed_fused(BR &b, uint32_t k, int32_t *row, int32_t (&h)[N], uint32_t 
     for (int j = 0; j < CH; j += 8) {
 #pragma unroll
         for (int t = 0; t < 8; t++) {
-            const uint32_t s = (uint32_t)rice_one(b, k, limit, trunc, &pw) + fixed_pred(h, t, order);
+            const uint32_t s = (uint32_t)rice_fused(b, rs, limit, trunc, &pw) + fixed_pred(h, t, order);
             h[t] = (int32_t)s;
             pw.v = (int32_t)(s << wasted);
             pw.at = row + (j + t) * RP;
@@ -1547,10 +1575,11 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : (MAXW == 16 ? 2 : 1
             rs.psamples = h.porder ? bs >> h.porder : bs - h.order;
             rs.plen = h.rice2 ? 5u : 4u;
             rs.pesc = h.rice2 ? 31u : 15u;
-            /* fused path: partition boundaries on chunk boundaries; the k_decode<8> instance
+            /* fused path: a chunk that lies inside one Rice partition (checked per chunk, so
+             * partitions need not be chunk-aligned: a chunk holding a partition boundary takes
+             * the generic path and the next one is fused again); the k_decode<8> instance
              * leaves 64-bit-accumulator subframes to the generic path (keeps it at 128 VGPRs) */
-            fast_ok = (h.type == T_FIXED || (h.type == T_LPC && (MAXW > 8 || h.path != P_WIDE))) &&
-                      (h.porder == 0 || (rs.psamples % CHK) == 0) && !(ablate & 12u);
+            fast_ok = (h.type == T_FIXED || (h.type == T_LPC && (MAXW > 8 || h.path != P_WIDE))) && !(ablate & 0x80Cu);
             /* MMX path keeps raw warm-ups for output: stash them in the rows of chunk 0 */
             if (h.type == T_LPC && h.path == P_MMX16) {
                 for (uint32_t t = 0; t < h.order; t++) row[t * RP] = warm[t];
@@ -1574,19 +1603,15 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : (MAXW == 16 ? 2 : 1
         const uint32_t nvalid = (active && n0 < bs) ? min((uint32_t)CHK, bs - n0) : 0u;
         const uint64_t ta = tnow(tmon);
         if (nvalid) {
-            bool fast = fast_ok && nvalid == CHK && n0 >= h.order;
-            if (fast && rs.left == 0) {
-                if (rs.pidx < rs.nparts) read_partition(b, rs);
-                else fast = false;
-            }
-            fast = fast && !rs.esc && rs.left >= CHK;
+            /* full chunks past the warm-up take the fused path; partition headers and escaped
+             * partitions are handled inside it (rice_fused) */
+            const bool fast = fast_ok && nvalid == CHK && n0 >= h.order;
             if (fast) {
                 STAT(b.stats, 0);
-                if (h.type == T_FIXED) fixed_fused<CHK>(b, rs.k, row, hh, h.order, h.wasted, limit, trunc);
-                else if (MAXW == 8 && h.path == P_MMX16) lpc_fused<CHK, 8, P_MMX16>(b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
-                else if (MAXW == 8) lpc_fused<CHK, 8, P_IA32>(b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
-                else LPC_DISPATCH(lpc_fused, b, rs.k, row, c, hh, ht, sh, h.wasted, limit, trunc);
-                rs.left -= CHK;
+                if (h.type == T_FIXED) fixed_fused<CHK>(b, rs, row, hh, h.order, h.wasted, limit, trunc);
+                else if (MAXW == 8 && h.path == P_MMX16) lpc_fused<CHK, 8, P_MMX16>(b, rs, row, c, hh, ht, sh, h.wasted, limit, trunc);
+                else if (MAXW == 8) lpc_fused<CHK, 8, P_IA32>(b, rs, row, c, hh, ht, sh, h.wasted, limit, trunc);
+                else LPC_DISPATCH(lpc_fused, b, rs, row, c, hh, ht, sh, h.wasted, limit, trunc);
             } else {
                 STAT(b.stats, 1);
                 if (h.type == T_FIXED || h.type == T_LPC || h.type == T_VERB) {

@@ -484,8 +484,9 @@ static uint32_t pick_bs(const bnsyn_params *p, rng_t *rng, uint32_t frame) {
 size_t bnsyn_max_bytes(const bnsyn_params *p) {
     uint64_t bs = p->variable_blocksize ? (p->bs_max ? p->bs_max : 65535) : p->blocksize;
     if (p->last_blocksize > bs) bs = p->last_blocksize;
-    /* verbatim worst case + escape slack + headers */
-    uint64_t per = (uint64_t)p->channels * (bs * (uint64_t)(p->bps + 2) / 8 + 64 + 4 * 32 + 16) + 64;
+    /* worst case: escaped partitions of FIXED-4 residuals (up to 16x the signal, +1 side bit:
+     * bps + 5 bits each) or verbatim, + headers; bps + 8 bits per sample covers both */
+    uint64_t per = (uint64_t)p->channels * (bs * (uint64_t)(p->bps + 8) / 8 + 64 + 4 * 32 + 16) + 64;
     return (size_t)(per * (uint64_t)p->nframes + 4096);
 }
 

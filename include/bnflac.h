@@ -174,7 +174,8 @@ BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uin
                                     uint64_t out_bytes, bnflac_frame_info *d_info, void *hip_stream);
 
 /* Timing experiments only: skip parts of the kernels (bit0 CRC-16, bit1 PCM stores,
- * bit2 restore, bit3 Rice decode, bit4 subframe walk).  Output is wrong while set. */
+ * bit2 restore, bit3 Rice decode, bit4 subframe walk).  Output is wrong while set.
+ * Exception: bit 0x800 only routes every k_decode chunk through the generic path (exact). */
 BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags);
 /* Mode switch (results stay exact): run the coalesced CRC-16 pass in bnflac_parse_frames'
  * launch (frame record crc_next) so the decode kernels skip their own CRC re-read for the

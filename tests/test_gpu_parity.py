@@ -753,3 +753,44 @@ def test_constant_last_subframe(gpu, kw):
     out, info, sp = _decode_batch(gpu, s.data.tobytes(), s.frame_offsets, libflac.OUT_INTERLEAVED32)
     assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all(), info[["status", "err", "flags"]]
     assert np.array_equal(out.view("<i4").reshape(-1, kw["channels"]), s.pcm)
+
+
+@pytest.mark.parametrize("bps,ch,stereo", [(16, 2, 0), (16, 2, 3), (24, 2, 1), (12, 1, 0), (20, 8, 0)])
+def test_loud_noisy_fixed4_escapes(gpu, bps, ch, stereo):
+    """Loud, noisy FIXED-4 (residuals up to 16x the signal): escaped partitions dominate and
+    partition boundaries fall anywhere -- the fused paths read partition headers and raw
+    escaped values inline.  Bit-exact against the oracle and the source PCM."""
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    p = synth.config("C2", channels=ch, bps=bps, subframe_mode=synth.SUB_FIXED, order=4, level=0.95, noise=0.3,
+                     stereo_mode=stereo, nframes=8, partition_order=-1, escape_permille=200, seed=40 + bps + ch)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    out, info, sp = _decode_batch(gpu, data, s.frame_offsets, libflac.OUT_INTERLEAVED32)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    pcm = out.view("<i4").reshape(-1, ch)
+    ev, opcm = oracle.run(data)
+    assert np.array_equal(pcm, oracle.interleave(ev, opcm))
+    assert np.array_equal(pcm, s.pcm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order,bs,porder", [(32, 512, 4), (32, 256, 3), (16, 256, 4), (8, 128, 4)])
+def test_empty_first_partition(gpu, order, bs, porder):
+    """LPC order == partition size: Rice partition 0 carries no samples, and the first
+    residual of the subframe sits in partition 1 (found by tools/stress.py: the fused path
+    must skip the empty partition's header).  Bit-exact against the oracle."""
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    p = synth.config("C2", channels=3, bps=16, subframe_mode=synth.SUB_LPC, order=order, blocksize=bs,
+                     last_blocksize=bs // 2, partition_order=porder, nframes=12, seed=700 + order)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    out, info, sp = _decode_batch(gpu, data, s.frame_offsets, libflac.OUT_INTERLEAVED32)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    pcm = out.view("<i4").reshape(-1, 3)
+    ev, opcm = oracle.run(data)
+    assert np.array_equal(pcm, oracle.interleave(ev, opcm))
+    assert np.array_equal(pcm, s.pcm)
