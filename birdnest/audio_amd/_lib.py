@@ -3,7 +3,8 @@ from __future__ import annotations
 
 import os
 
-LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+# BNFLAC_LIB_DIR: a development build variant instead (build.py BNFLAC_VARIANT_DIR)
+LIB_DIR = os.environ.get("BNFLAC_LIB_DIR") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 
 
 def lib_path(name: str) -> str:

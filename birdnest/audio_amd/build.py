@@ -44,13 +44,21 @@ KERNEL_TUS = (0, 1, 2, 3, 4, 5)  # one build of bnflac_kernels.hip per BNF_TU: s
 
 
 def build_hip(force=False, verbose=False):
-    """Compile the kernel TUs and the runtime in parallel (hipcc -c), then link."""
-    out = os.path.join(LIB, "libbnflac.so")
+    """Compile the kernel TUs and the runtime in parallel (hipcc -c), then link.
+
+    Development variants (never the product): BNFLAC_VARIANT_DIR=<dir> builds into <dir>
+    (objects in <dir>/build) with the extra hipcc flags in BNFLAC_EXTRA_CFLAGS, e.g.
+    -DBNFLAC_PHASE_TIMERS; load it with BNFLAC_LIB_DIR=<dir> in the debug tools."""
+    vdir = os.environ.get("BNFLAC_VARIANT_DIR")
+    libdir = vdir or LIB
+    out = os.path.join(libdir, "libbnflac.so")
     if force or _stale(out, HIP_SOURCES + HIP_HEADERS):
-        os.makedirs(LIB, exist_ok=True)
-        objdir = os.path.join(PKG, "build")
+        os.makedirs(libdir, exist_ok=True)
+        objdir = os.path.join(vdir, "build") if vdir else os.path.join(PKG, "build")
         os.makedirs(objdir, exist_ok=True)
         base = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-I" + INCLUDE]
+        if vdir:
+            base += os.environ.get("BNFLAC_EXTRA_CFLAGS", "").split()
         jobs, objs = [], []
         # development shortcut: BNFLAC_DEV_TUS="1,3" recompiles only those kernel TUs and
         # reuses the other objects as they are (never set for a real build)

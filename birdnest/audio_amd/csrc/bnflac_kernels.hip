@@ -87,9 +87,13 @@ DEV uint64_t lds_ld64(const void *a) {
     return v;
 }
 typedef __attribute__((address_space(1))) const void gvoid;
+/* 16-byte global store through an integer address: the address-space cast keeps it a
+ * global_store (a generic pointer would make it a flat store, which also counts in
+ * lgkmcnt -- every later LDS wait would then wait for the HBM write) */
+DEV void gst128(uint64_t addr, u32x4 v) { *(__attribute__((address_space(1))) u32x4 *)addr = v; }
 
 /* ----------------------------------------------------------------- bit reader */
-#define RING_MAX 8        /* 16-byte slots per lane (k_parse; k_decode<8> uses 4) */
+#define RING_MAX 16       /* 16-byte slots per lane (k_parse and k_decode_st use 8) */
 #define RING_LANE_DW 256  /* dwords per slot row (64 lanes x 4) */
 
 /* MSB-first bit stream.  Window hi:lo (big-endian words); the cursor is 32-s bits into
@@ -167,7 +171,7 @@ DEV void br_refill(BR &b) {
      * line) refills from the cursor's block instead */
     const uint32_t need = b.rdepth >= 8u ? ((b.wi >> 2) & ~3u) : (b.wi >> 2);
     const uint32_t lo = max(b.iend, need), hi = need + b.rdepth;
-#pragma unroll
+#pragma unroll 1 /* rare path (seeks, landings), inlined at every cursor advance: keep it small */
     for (int s = 0; s < RING_MAX; s++) {
         if ((uint32_t)s >= b.rdepth) break; /* wave-uniform */
         const uint32_t j = lo + (((uint32_t)s - lo) & (b.rdepth - 1u));
@@ -182,11 +186,11 @@ DEV void br_drained(BR &b) { /* every vector-memory op of this wave has complete
     b.vendw = b.iend * 4u;
     b.iend_old = b.iend;
 }
-DEV void br_land(BR &b) {
+DEV void br_land(BR &b, uint32_t margin = 0) { /* afterwards words wi .. wi + margin have landed */
     STAT(b.stats, 2);
     wait_vm();
     br_drained(b);
-    if (b.wi >= b.vendw) {
+    if (b.wi + margin >= b.vendw) {
         br_refill(b);
         wait_vm();
         br_drained(b);
@@ -248,6 +252,33 @@ DEV void br_refill2(BR &b, bool want, VmQ &q, bool nowait = false) {
     q.d_last = d;
 }
 
+/* k_decode's refill (1-deep): br_issue, after a chunk's entropy phase, fetches the 16-byte
+ * blocks up to rdepth past the block of the cursor word (never that block's slot, which
+ * br_adv re-reads), so at least (rdepth - 1) * 16 bytes lie ahead of the cursor; br_wait1,
+ * before the next entropy phase, waits for them -- only the PCM stores packed since (at
+ * least q.s_last of them, all younger) may stay in flight -- and marks them landed.  The
+ * restore and the pack run in between.  A lane that needs more within one chunk lands
+ * (br_land). */
+DEV void br_wait1(BR &b, VmQ &q) {
+    wait_vm_n(q.s_last);
+    b.vendw = b.iend * 4u;
+    q.s_last = 0;
+}
+DEV void br_issue(BR &b, bool want) {
+    const uint32_t cb = b.wi >> 2;
+    const uint32_t lo = max(b.iend, cb), hi = cb + b.rdepth;
+#pragma unroll
+    for (int k = 0; k < RING_MAX; k++) {
+        if ((uint32_t)k >= b.rdepth) break; /* wave-uniform */
+        const uint32_t j = lo + (((uint32_t)k - lo) & (b.rdepth - 1u)); /* the block for slot k */
+        const bool go = want && j < hi;
+        if (__any(go)) {
+            if (go) dma_block(b, j, (uint32_t)k);
+        }
+    }
+    if (want) b.iend = max(b.iend, hi);
+}
+
 DEV uint64_t br_pos(const BR &b) { return ((uint64_t)(b.wi - 1u) << 5) - b.s; }
 DEV uint32_t br_peek(const BR &b) { return __builtin_amdgcn_alignbit(b.hi, b.lo, b.s); }
 /* Pending LDS store carried into the next cursor advance (fused decode): issuing it after
@@ -284,13 +315,15 @@ DEV void br_adv(BR &b, uint32_t n, PendW *pw = nullptr) { /* n <= 32; branch-fre
     asm volatile("" : "+v"(off) : "v"(b.lo));
     b.nx = b.lring[off];
 }
+template <bool CHECK = true>
 DEV uint32_t br_read(BR &b, uint32_t n) { /* 0..32 bits */
     uint32_t v = n ? (br_peek(b) >> ((32u - n) & 31u)) : 0u;
-    br_adv(b, n);
+    br_adv<CHECK>(b, n);
     return v;
 }
+template <bool CHECK = true>
 DEV int32_t br_read_s(BR &b, uint32_t n) {
-    uint32_t v = br_read(b, n);
+    uint32_t v = br_read<CHECK>(b, n);
     uint32_t s = (32u - n) & 31u;
     return (int32_t)(v << s) >> s;
 }
@@ -495,9 +528,10 @@ struct SubHdr {
 };
 
 /* read_subframe_ @0x10012480 up to (and including) the residual coding header.
- * warm/coef receive up to 32 values.  Returns BNF_ST_*; on ERROR sets err and the
- * reader position is where libFLAC stops. */
-template <bool STORE, int NW = 32>
+ * STORE: warm-ups go to warm[u * WS] and coefficients to coef[u] for u < NW, in loops
+ * unrolled to NW (compile-time indices: register arrays stay in registers).  Returns
+ * BNF_ST_*; on ERROR sets err and the reader position is where libFLAC stops. */
+template <bool STORE, int NW = 32, int WS = 1>
 DEV uint32_t parse_subframe_head(BR &b, uint32_t bps, uint32_t bs, uint64_t limit, SubHdr &h,
                                  int32_t *warm, int32_t *coef, int32_t &err) {
     uint32_t x = br_read(b, 8);
@@ -535,18 +569,26 @@ DEV uint32_t parse_subframe_head(BR &b, uint32_t bps, uint32_t bs, uint64_t limi
         h.type = T_LPC;
         h.order = ((x >> 1) & 31u) + 1u;
     }
-    for (uint32_t u = 0; u < h.order; u++) {
-        int32_t v = br_read_s(b, bps);
-        if (STORE && u < (uint32_t)NW) warm[u] = v;
+    if (STORE) {
+#pragma unroll
+        for (int u = 0; u < NW; u++)
+            if ((uint32_t)u < h.order) warm[u * WS] = br_read_s(b, bps);
+        for (uint32_t u = NW; u < h.order; u++) br_read_s(b, bps);
+    } else {
+        for (uint32_t u = 0; u < h.order; u++) br_read_s(b, bps);
     }
     if (h.type == T_LPC) {
         uint32_t p = br_read(b, 4);
         if (p == 15) { err = E_LOST_SYNC; return BNF_ST_ERROR; }
         h.prec = p + 1;
         h.shift = br_read_s(b, 5);
-        for (uint32_t u = 0; u < h.order; u++) {
-            int32_t v = br_read_s(b, h.prec);
-            if (STORE && u < (uint32_t)NW) coef[u] = v;
+        if (STORE) {
+#pragma unroll
+            for (int u = 0; u < NW; u++)
+                if ((uint32_t)u < h.order) coef[u] = br_read_s(b, h.prec);
+            for (uint32_t u = NW; u < h.order; u++) br_read_s(b, h.prec);
+        } else {
+            for (uint32_t u = 0; u < h.order; u++) br_read_s(b, h.prec);
         }
         uint32_t ilog = 31u - (uint32_t)__builtin_clz(h.order);
         if (bps + h.prec + ilog <= 32) h.path = (bps <= 16 && h.prec <= 16 && h.order >= 4) ? P_MMX16 : P_IA32;
@@ -825,14 +867,15 @@ struct RS { /* residual reader state */
 };
 
 /* Rice partition header (read_residual_partitioned_rice_ @0x10012da0) */
+template <bool CHECK = true>
 DEV void read_partition(BR &b, RS &s) {
-    const uint32_t kk = br_read(b, s.plen);
+    const uint32_t kk = br_read<CHECK>(b, s.plen);
     s.left = (s.porder == 0 || s.pidx > 0) ? s.psamples : s.psamples - s.order;
     if (kk < s.pesc) {
         s.k = kk;
         s.esc = 0;
     } else {
-        s.k = br_read(b, 5);
+        s.k = br_read<CHECK>(b, 5);
         s.esc = 1;
     }
     s.pidx++;
@@ -840,6 +883,7 @@ DEV void read_partition(BR &b, RS &s) {
 
 /* One Rice codeword (the block reader @0x10001b30/@0x1001aed0: u = (q << k) | lsb in
  * 32-bit unsigned, zig-zag). */
+template <bool CHECK = true> /* false: the caller made sure the ring holds the word this reads */
 DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc, PendW *pw = nullptr) {
     const uint32_t w = br_peek(b);
     /* v_ffbh gives ~0u for w == 0, which fails the unsigned test below like any prefix
@@ -848,7 +892,7 @@ DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc, PendW *
     const bool fast = q0 <= 31u - k;
     uint32_t u = (q0 << k) | __builtin_amdgcn_ubfe(w, 31u - k - q0, k);
     const bool slow = any_lane(!fast); /* wave-uniform, taken before the advance (stays in SGPRs) */
-    br_adv(b, fast ? q0 + 1u + k : 0u, pw);
+    br_adv<CHECK>(b, fast ? q0 + 1u + k : 0u, pw);
     if (__builtin_expect(slow, 0)) { /* the work is per lane */
         STAT(b.stats, 3);
         if (!fast) { /* long unary prefix: read_unary_unsigned, then the k low bits */
@@ -860,28 +904,23 @@ DEV int32_t rice_one(BR &b, uint32_t k, uint64_t limit, uint32_t &trunc, PendW *
     return (int32_t)((u >> 1) ^ (0u - (u & 1u)));
 }
 
-/* next residual of the generic path */
-DEV int32_t next_val(BR &b, RS &s, uint64_t limit, uint32_t &trunc) {
-    if (s.verb) return br_read_s(b, s.k);
-    while (s.left == 0) {
-        if (s.pidx >= s.nparts) { trunc = 1; return 0; }
-        read_partition(b, s);
-    }
-    s.left--;
-    if (s.esc) return br_read_s(b, s.k);
-    return rice_one(b, s.k, limit, trunc);
-}
-
 /* next residual on the fused paths: a new partition's header and escaped (raw) partitions
  * inline behind wave-uniform tests, so a chunk need not lie inside one partition; Rice
  * codewords as rice_one.  An escaped lane issues its pending row write itself. */
 DEV int32_t rice_fused(BR &b, RS &rs, uint64_t limit, uint32_t &trunc, PendW *pw) {
+    /* one landing check per residual: with words wi .. wi+2 in the landed ring, the up to two
+     * partition headers and one value below (<= 49 bits) advance unchecked; only a long
+     * unary prefix (rice_one's slow path) reads on with checks */
+    if (__builtin_expect(any_lane(b.wi + 2u >= b.vendw), 0)) {
+        br_land(b, 2u);
+        b.nx = ring_word(b, b.wi);
+    }
     const bool np = rs.left == 0;
     if (__builtin_expect(any_lane(np), 0)) {
         if (np) {
             do { /* partition 0 holds no samples when the order equals the partition size */
                 if (rs.pidx < rs.nparts) {
-                    read_partition(b, rs);
+                    read_partition<false>(b, rs);
                 } else { /* more samples than the partitions carry: a damaged frame */
                     trunc = 1;
                     rs.left = 0x7fffffffu;
@@ -894,10 +933,10 @@ DEV int32_t rice_fused(BR &b, RS &rs, uint64_t limit, uint32_t &trunc, PendW *pw
         if (rs.esc) {
             if (pw && pw->on) *pw->at = pw->v;
             if (pw) pw->on = false;
-            return br_read_s(b, rs.k);
+            return br_read_s<false>(b, rs.k);
         }
     }
-    return rice_one(b, rs.k, limit, trunc, pw);
+    return rice_one<false>(b, rs.k, limit, trunc, pw);
 }
 
 DEV void finish_partitions(BR &b, RS &s) {
@@ -909,175 +948,99 @@ DEV void finish_partitions(BR &b, RS &s) {
     }
 }
 
-/* saturate to int16 (packssdw); the int16 round trip tells the compiler the value is a
- * sign-extended 16-bit quantity, so v_mul_i32_i24 needs no re-extension */
+/* saturate to int16 (packssdw) / the low 16 bits as int16 (MMX16 history words) */
 DEV int32_t sat16(int32_t x) { return (int32_t)(int16_t)min(max(x, -32768), 32767); }
 DEV int32_t tr16(int32_t x) { return (int32_t)(int16_t)(uint16_t)(uint32_t)x; }
-/* low 32 bits of (sext24(a) * sext24(b)): one v_mul_i32_i24.  Written as asm because the
- * C form ((a << 8) >> 8) * ((b << 8) >> 8) keeps a v_bfe per operand whenever the compiler
- * cannot prove the operand already fits 24 bits (loop-carried history values). */
-DEV int32_t mul24(int32_t a, int32_t b) {
-    int32_t r;
-    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
+/* ---------------------------------------------------------------- k_decode restore
+ * Every subframe type is restored as one linear predictor over 32-bit samples, so a wave
+ * whose lanes hold different types and libFLAC paths runs ONE instruction stream:
+ *   - libFLAC's 32-bit paths (the ia32 routine @0x1001be10, the MMX16 one @0x1001c000)
+ *     both compute the low 32 bits of sum c[t] * x[t] -- MMX16 on history that is saturated
+ *     to int16 (taps 4..) or truncated to int16 (taps 0..3, the last pmaddwd pair), ia32 in
+ *     int32 wrap -- and shift that (psrad: >= 32 -> 31; sar: & 31);
+ *   - the 64-bit path (FLAC__lpc_restore_signal_wide @0x10006120) shifts the exact sum;
+ *   - FIXED order o (FLAC__fixed_restore_signal @0x10003810, int32 wrap) is LPC with coefficients
+ *     1 | 2,-1 | 3,-3,1 | 4,-6,4,-1 and shift 0; CONSTANT is order 1, coefficient 1,
+ *     warm-up cval and zero residuals; VERBATIM is order 0 with the raw values as residuals.
+ * Per sample: W exact 64-bit MACs (v_mad_i64_i32, tools/ubench_mad.hip) in two chains, the
+ * history in a register ring with compile-time indices (W samples unrolled by recursion). */
+struct Pred {
+    int32_t sh;       /* effective shift of the lane's path */
+    uint32_t order;   /* samples before it are warm-ups (raw in the rows) */
+    uint32_t wasted;  /* output = sample << wasted */
+    bool mmx, wide;
+};
+
+/* the prediction of the sample at ring position T from the W history values */
+template <int T, int W>
+DEV int32_t pred_at(const int32_t (&c)[W], const int32_t (&x)[W], const int32_t (&xt)[4], const Pred &p) {
+    int64_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int t = 0; t < W; t++) {
+        const int32_t hv = (t < 4) ? xt[(T - 1 - t) & 3] : x[((T - 1 - t) % W + W) % W];
+        if (t & 1) s1 += (int64_t)c[t] * (int64_t)hv;
+        else s0 += (int64_t)c[t] * (int64_t)hv;
+    }
+    /* keep the two MAC chains apart (the compiler would re-associate them into one) */
+    asm volatile("" : "+v"(s0), "+v"(s1));
+    const int64_t S = s0 + s1;
+    return p.wide ? (int32_t)(S >> p.sh) : ((int32_t)S >> p.sh);
 }
-/* acc + low 32 bits of (sext24(a) * sext24(b)): one v_mad_i32_i24 (32-bit wrap add) */
-DEV int32_t mad24(int32_t a, int32_t b, int32_t acc) {
-    int32_t r;
-    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(acc));
-    return r;
+template <int T, int W>
+DEV void push_at(int32_t (&x)[W], int32_t (&xt)[4], const Pred &p, int32_t s) {
+    x[T % W] = p.mmx ? sat16(s) : s;
+    xt[T & 3] = p.mmx ? tr16(s) : s;
 }
 
-/* LPC prediction for the sample at ring position i (compile-time), libFLAC path P.
- * sh is the path's effective shift (MMX psrad: >= 32 -> 31; ia32 sar: & 31; 64-bit
- * _allshr: & 0xFF, >= 64 -> 63). */
-template <int W, int P, int N>
-DEV int32_t lpc_pred(const int32_t (&c)[N], const int32_t (&h)[N], const int32_t (&ht)[4], int i, int32_t sh) {
-    if (P == P_MMX16) {
-        int32_t sum = 0;
-#pragma unroll
-        for (int t = 0; t < W; t++) {
-            const int32_t hv = (t < 4) ? ht[(i - 1 - t) & 3] : h[((i - 1 - t) % W + W) % W];
-            sum = t ? mad24(c[t], hv, sum) : mul24(c[t], hv);
-        }
-        return sum >> sh;
-    } else if (P == P_IA32) {
-        /* exact int32 wrap product via 12-bit split: c*s = (c*(s>>12) << 12) + c*(s&0xfff) */
-        int32_t shi = 0, slo = 0;
-#pragma unroll
-        for (int t = 0; t < W; t++) {
-            const int32_t hv = h[((i - 1 - t) % W + W) % W];
-            shi = t ? mad24(c[t], hv >> 12, shi) : mul24(c[t], hv >> 12);
-            slo = t ? mad24(c[t], hv & 0xfff, slo) : mul24(c[t], hv & 0xfff);
-        }
-        const int32_t sum = (int32_t)(((uint32_t)shi << 12) + (uint32_t)slo);
-        return sum >> sh;
-    } else {
-        /* exact 64-bit products (v_mad_i64_i32, as fast as v_mad_i32_i24 on gfx950:
-         * tools/ubench_mad.hip) in two independent chains: the dependent-MAC latency
-         * (~12 cycles), not the issue rate, bounds a lane-per-subframe kernel */
-        int64_t s2[2] = {0, 0};
-#pragma unroll
-        for (int t = 0; t < W; t++) s2[t & 1] += (int64_t)c[t] * (int64_t)h[((i - 1 - t) % W + W) % W];
-        return (int32_t)((s2[0] + s2[1]) >> sh);
+/* split path, samples T..W-1 of the W-sample group at row j (rows hold warm-ups /
+ * residuals on entry, output samples on exit); n = subframe sample index of row j */
+template <int T, int W>
+DEV void restore_steps(int32_t *row, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4], const Pred &p,
+                       uint32_t n, uint32_t nv, uint32_t j) {
+    if constexpr (T < W) {
+        const int32_t v = row[(j + T) * RP];
+        const int32_t pr = pred_at<T, W>(c, x, xt, p);
+        const int32_t s = (n + (uint32_t)T < p.order) ? v : (int32_t)((uint32_t)v + (uint32_t)pr);
+        push_at<T, W>(x, xt, p, s);
+        if (j + (uint32_t)T < nv) row[(j + T) * RP] = (int32_t)((uint32_t)s << p.wasted);
+        restore_steps<T + 1, W>(row, c, x, xt, p, n, nv, j);
     }
 }
 
-template <int W, int P, int N>
-DEV void lpc_push(int32_t (&h)[N], int32_t (&ht)[4], int i, int32_t s) {
-    if (P == P_MMX16) {
-        ht[i & 3] = tr16(s);
-        h[i % W] = sat16(s);
-    } else {
-        h[i % W] = s;
-    }
-}
-
-/* Generic LPC restore of one chunk (rows hold residuals on entry, samples << wasted on
- * exit); handles warm-up samples and short chunks. */
-template <int CH, int W, int P, int N>
-DEV void lpc_chunk(int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4], uint32_t n0,
-                   uint32_t nvalid, uint32_t order, int32_t sh, uint32_t wasted) {
-#pragma unroll
-    for (int i = 0; i < CH; i++) {
-        const uint32_t n = n0 + (uint32_t)i;
-        if ((uint32_t)i < nvalid) {
-            int32_t s;
-            if (n < order) {
-                s = h[i % W];
-                if (P == P_MMX16) s = row[i * RP]; /* raw warm-up kept in the row */
-            } else {
-                s = (int32_t)((uint32_t)row[i * RP] + (uint32_t)lpc_pred<W, P>(c, h, ht, i, sh));
-                if (P == P_MMX16) ht[i & 3] = tr16(s);
-            }
-            if (P == P_MMX16) h[i % W] = sat16(s);
-            else h[i % W] = s;
-            row[i * RP] = (int32_t)((uint32_t)s << wasted);
-        }
-    }
-}
-
-/* Fused Rice decode + LPC restore of a full chunk past the warm-up, inside one Rice
- * partition (parameter k, not escaped): the residual never leaves registers and the
- * two dependency chains (bit cursor, predictor) interleave. */
-/* samples T..W-1 of one W-sample group, unrolled by recursion so every history index is a
- * compile-time constant (a rolled loop puts the ring behind s_set_gpr_idx moves) */
-template <int T, int W, int P, int N>
-DEV void lpc_fused_steps(BR &b, RS &rs, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
-                         int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc, PendW &pw, int j) {
+/* fused path (a full chunk past the warm-up): each residual goes from the bit reader
+ * straight into the predictor, so the bit-cursor chain and the MAC chains of neighbouring
+ * samples overlap; each row write is issued in the next codeword's cursor advance */
+template <int T, int W>
+DEV void fused_steps(BR &b, RS &rs, int32_t *row, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4],
+                     const Pred &p, uint64_t limit, uint32_t &trunc, PendW &pw, uint32_t j) {
     if constexpr (T < W) {
         const int32_t r = rice_fused(b, rs, limit, trunc, &pw);
-        const int32_t s = (int32_t)((uint32_t)r + (uint32_t)lpc_pred<W, P>(c, h, ht, T, sh));
-        lpc_push<W, P>(h, ht, T, s);
-        pw.v = (int32_t)((uint32_t)s << wasted);
+        const int32_t s = (int32_t)((uint32_t)r + (uint32_t)pred_at<T, W>(c, x, xt, p));
+        push_at<T, W>(x, xt, p, s);
+        pw.v = (int32_t)((uint32_t)s << p.wasted);
         pw.at = row + (j + T) * RP;
         pw.on = true;
-        lpc_fused_steps<T + 1, W, P, N>(b, rs, row, c, h, ht, sh, wasted, limit, trunc, pw, j);
+        fused_steps<T + 1, W>(b, rs, row, c, x, xt, p, limit, trunc, pw, j);
     }
 }
-
-template <int CH, int W, int P, int N>
-DEV void lpc_fused(BR &b, RS &rs, int32_t *row, const int32_t (&c)[N], int32_t (&h)[N], int32_t (&ht)[4],
-                   int32_t sh, uint32_t wasted, uint64_t limit, uint32_t &trunc) {
-    /* each sample's row write is issued just before the next codeword's ring read, so the
-     * next LDS wait (hipcc waits lgkmcnt(0) here) finds every LDS op a codeword old */
+template <int CH, int W>
+DEV void fused_chunk(BR &b, RS &rs, int32_t *row, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4],
+                     const Pred &p, uint64_t limit, uint32_t &trunc) {
     PendW pw;
     pw.at = row;
     pw.v = 0;
     pw.on = false;
 #pragma unroll 1
-    for (int j = 0; j < CH; j += W) lpc_fused_steps<0, W, P, N>(b, rs, row, c, h, ht, sh, wasted, limit, trunc, pw, j);
+    for (uint32_t j = 0; j < (uint32_t)CH; j += W) fused_steps<0, W>(b, rs, row, c, x, xt, p, limit, trunc, pw, j);
     *pw.at = pw.v;
 }
 
-/* FLAC__fixed_restore_signal @0x10003810 (ring of 8, 32-bit wrap) */
-template <int N>
-DEV uint32_t fixed_pred(const int32_t (&h)[N], int i, uint32_t order) {
-    const uint32_t a = (uint32_t)h[(i - 1) & 7], bb = (uint32_t)h[(i - 2) & 7], c = (uint32_t)h[(i - 3) & 7],
-                   d = (uint32_t)h[(i - 4) & 7];
-    switch (order) {
-    case 0: return 0;
-    case 1: return a;
-    case 2: return (a << 1) - bb;
-    case 3: return (((a - bb) << 1) + (a - bb)) + c;
-    default: return ((a + c) << 2) - ((bb << 2) + (bb << 1)) - d;
-    }
-}
-
-template <int CH, int N>
-DEV void fixed_chunk(int32_t *row, int32_t (&h)[N], uint32_t n0, uint32_t nvalid, uint32_t order, uint32_t wasted) {
-#pragma unroll
-    for (int i = 0; i < CH; i++) {
-        const uint32_t n = n0 + (uint32_t)i;
-        if ((uint32_t)i < nvalid) {
-            uint32_t s;
-            if (n < order) s = (uint32_t)h[i & 7];
-            else s = (uint32_t)row[i * RP] + fixed_pred(h, i, order);
-            h[i & 7] = (int32_t)s;
-            row[i * RP] = (int32_t)(s << wasted);
-        }
-    }
-}
-
-template <int CH, int N>
-DEV void fixed_fused(BR &b, RS &rs, int32_t *row, int32_t (&h)[N], uint32_t order, uint32_t wasted,
-                     uint64_t limit, uint32_t &trunc) {
-    PendW pw;
-    pw.at = row;
-    pw.v = 0;
-    pw.on = false;
+/* restore one chunk of CH rows (nv of them valid), W-sample groups */
+template <int CH, int W>
+DEV void restore_chunk(int32_t *row, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4], const Pred &p,
+                       uint32_t n0, uint32_t nv) {
 #pragma unroll 1
-    for (int j = 0; j < CH; j += 8) {
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const uint32_t s = (uint32_t)rice_fused(b, rs, limit, trunc, &pw) + fixed_pred(h, t, order);
-            h[t] = (int32_t)s;
-            pw.v = (int32_t)(s << wasted);
-            pw.at = row + (j + t) * RP;
-            pw.on = true;
-        }
-    }
-    *pw.at = pw.v;
+    for (uint32_t j = 0; j < (uint32_t)CH; j += W) restore_steps<0, W>(row, c, x, xt, p, n0 + j, nv, j);
 }
 
 /* CRC-16 (poly 0x8005) over bytes [b0, b1), slice-by-8 with the tables in LDS. */
@@ -1271,8 +1234,9 @@ template <int FMT, int CH>
 DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, uint32_t n0, bool fok, uint32_t bs,
                        uint32_t C, uint32_t as, uint64_t os, uint32_t stream_channels, uint32_t fr_bytes,
                        uint8_t *__restrict__ out) {
-    const uint32_t per = CH / chn_lanes;
-    const uint32_t fl = lane / chn_lanes, part = lane % chn_lanes;
+    const uint32_t lg = __builtin_ctz(chn_lanes); /* a power of 2 (lanes_for) */
+    const uint32_t per = (uint32_t)CH >> lg;
+    const uint32_t fl = lane >> lg, part = lane & (chn_lanes - 1u);
     const uint32_t i0 = part * per;
     if (!fok || n0 + i0 >= bs) return 0;
     const uint32_t cnt = min(per, bs - (n0 + i0));
@@ -1297,13 +1261,13 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
                 decorrelate(as, l[q], r[q]);
             }
             if (FMT == BNF_OUT_FLACDECODER) { /* FLACDecoder.cs:543-562: L | R << 16 */
-                *(uint4 *)(base + i * 4u) = make_uint4(((uint32_t)l[0] & 0xffffu) | ((uint32_t)r[0] << 16),
-                                                       ((uint32_t)l[1] & 0xffffu) | ((uint32_t)r[1] << 16),
-                                                       ((uint32_t)l[2] & 0xffffu) | ((uint32_t)r[2] << 16),
-                                                       ((uint32_t)l[3] & 0xffffu) | ((uint32_t)r[3] << 16));
+                gst128(base + i * 4u, u32x4{((uint32_t)l[0] & 0xffffu) | ((uint32_t)r[0] << 16),
+                                            ((uint32_t)l[1] & 0xffffu) | ((uint32_t)r[1] << 16),
+                                            ((uint32_t)l[2] & 0xffffu) | ((uint32_t)r[2] << 16),
+                                            ((uint32_t)l[3] & 0xffffu) | ((uint32_t)r[3] << 16)});
             } else {
-                *(int4 *)(base + i * 8u) = make_int4(l[0], r[0], l[1], r[1]);
-                *(int4 *)(base + i * 8u + 16u) = make_int4(l[2], r[2], l[3], r[3]);
+                gst128(base + i * 8u, u32x4{(uint32_t)l[0], (uint32_t)r[0], (uint32_t)l[1], (uint32_t)r[1]});
+                gst128(base + i * 8u + 16u, u32x4{(uint32_t)l[2], (uint32_t)r[2], (uint32_t)l[3], (uint32_t)r[3]});
             }
         }
         return pack_fast_stores<FMT, CH>();
@@ -1321,15 +1285,15 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
         if (a16 || a4) {
             /* the run's dwords in registers (compile-time indices: up to CH/4 groups of fb) */
             uint32_t dw[CH / 4 * 3];
+            uint32_t q = 0, c = 0; /* sample and channel of value k = q * C + c (no division) */
 #pragma unroll
             for (int g = 0; g < CH / 4; g++) {
                 int32_t v[4] = {0, 0, 0, 0};
                 if ((uint32_t)g < ngrp) {
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        const uint32_t k = 4u * g + (uint32_t)u;
-                        const uint32_t q = k / C, c = k - q * C;
                         v[u] = rows[q * RP + c];
+                        if (++c == C) { c = 0; q++; }
                     }
                     if (C == 2) { /* stereo pairs are whole within a group of 4 */
                         decorrelate(as, v[0], v[1]);
@@ -1428,7 +1392,7 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
     } while (0)
 
 template <int MAXW, int CHK, int RD>
-__global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : (MAXW == 16 ? 2 : 1)) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
+__global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
                                                       uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                       int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
                                                       bnf_frame_info *__restrict__ info, uint32_t ablate) {
@@ -1445,8 +1409,9 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : (MAXW == 16 ? 2 : 1
     uint64_t *t_out = (uint64_t *)(t_bs + 320);
 
     const uint32_t lane = threadIdx.x;
-    const uint32_t fpb = DEC_LANES / chn_lanes;
-    const uint32_t fl = lane / chn_lanes, ch = lane % chn_lanes;
+    const uint32_t lg = __builtin_ctz(chn_lanes); /* a power of 2 (lanes_for) */
+    const uint32_t fpb = DEC_LANES >> lg;
+    const uint32_t fl = lane >> lg, ch = lane & (chn_lanes - 1u);
     const uint32_t f = blockIdx.x * fpb + fl;
     const uint64_t limit = nbytes * 8u;
 
@@ -1526,64 +1491,64 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : (MAXW == 16 ? 2 : 1
     RS rs;
     rs.verb = 0; rs.k = 0; rs.esc = 0; rs.left = 0; rs.pidx = 0; rs.nparts = 0; rs.psamples = 0;
     rs.order = 0; rs.plen = 4; rs.pesc = 15; rs.porder = 0;
-    int32_t c[MAXW], hh[MAXW], ht[4];
+    int32_t c[MAXW], x[MAXW], xt[4]; /* coefficients; history ring (MMX16: int16 words) */
 #pragma unroll
-    for (int t = 0; t < MAXW; t++) { c[t] = 0; hh[t] = 0; }
+    for (int t = 0; t < MAXW; t++) { c[t] = 0; x[t] = 0; }
 #pragma unroll
-    for (int t = 0; t < 4; t++) ht[t] = 0;
+    for (int t = 0; t < 4; t++) xt[t] = 0;
+    Pred pd;
+    pd.sh = 0; pd.order = 0; pd.wasted = 0; pd.mmx = false; pd.wide = false;
     uint32_t trunc = 0, st = BNF_ST_OK;
     int32_t err = -1;
     uint32_t bs = 0;
-    int32_t sh = 0;
-    bool fast_ok = false;
     int32_t *row = lds + lane;
     if (active) {
         bs = fi.blocksize;
         /* read from HBM: indexing the local record by the runtime channel would spill it to scratch */
         br_seek(b, fi.frame_off * 8u + info[f].sub_start[ch]);
-        int32_t warm[MAXW], coef[MAXW]; /* orders above MAXW are rejected below */
-        st = parse_subframe_head<true, MAXW>(b, sub_bps(fi, ch), bs, limit, h, warm, coef, err);
+        int32_t coef[MAXW]; /* orders above MAXW are rejected below */
+        /* warm-ups go straight to the rows of chunk 0: raw, they are output samples */
+        st = parse_subframe_head<true, MAXW, RP>(b, sub_bps(fi, ch), bs, limit, h, row, coef, err);
         if (st == BNF_ST_OK && h.type == T_LPC && h.order > MAXW) {
             st = BNF_ST_ERROR; /* k_parse mis-flagged: cannot happen for the subframes it read */
             err = E_UNPARSEABLE;
         }
         if (st == BNF_ST_OK) {
-            /* coefficients / history into registers (compile-time indices only) */
-#pragma unroll
-            for (int t = 0; t < MAXW; t++) {
-                const bool in = (uint32_t)t < h.order;
-                c[t] = (in && h.type == T_LPC) ? coef[t] : 0;
-                const int32_t wv = in ? warm[t] : 0;
-                hh[t] = (h.type == T_LPC && h.path == P_MMX16) ? sat16(wv) : wv;
-            }
-            if (h.type == T_LPC && h.path == P_MMX16) {
-#pragma unroll
-                for (int t = 0; t < MAXW; t++)
-                    if ((uint32_t)t < h.order && (uint32_t)t + 4u >= h.order) ht[t & 3] = sat16(warm[t]);
-            }
+            /* the subframe as a linear predictor (see Pred) */
+            pd.order = h.order;
+            pd.wasted = h.wasted;
             if (h.type == T_LPC) {
-                if (h.path == P_MMX16) sh = ((uint32_t)h.shift >= 32u) ? 31 : h.shift;
-                else if (h.path == P_IA32) sh = h.shift & 31;
-                else sh = min((uint32_t)h.shift & 0xFFu, 63u);
+#pragma unroll
+                for (int t = 0; t < MAXW; t++) c[t] = ((uint32_t)t < h.order) ? coef[t] : 0;
+                pd.mmx = h.path == P_MMX16;
+                pd.wide = h.path == P_WIDE;
+                if (h.path == P_MMX16) pd.sh = ((uint32_t)h.shift >= 32u) ? 31 : h.shift;
+                else if (h.path == P_IA32) pd.sh = h.shift & 31;
+                else pd.sh = min((uint32_t)h.shift & 0xFFu, 63u);
+            } else if (h.type == T_FIXED) {
+                const uint32_t o = h.order;
+                c[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
+                c[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
+                c[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
+                c[3] = o == 4 ? -1 : 0;
+            } else if (h.type == T_CONST) {
+                c[0] = 1;
+                pd.order = 1;
+                row[0] = h.cval;
             }
-            rs.verb = (h.type == T_VERB);
-            rs.k = h.bps;
+            /* residual reader: FIXED / LPC partitioned Rice; VERBATIM as one endless escaped
+             * partition of bps-bit raw values; CONSTANT the same with 0-bit values (no bits) */
+            const bool rice = h.type == T_FIXED || h.type == T_LPC;
+            rs.verb = rice ? 0u : 1u; /* no partition headers to finish */
+            rs.esc = rice ? 0u : 1u;
+            rs.k = h.type == T_VERB ? h.bps : 0u;
+            rs.left = rice ? 0u : 0x7fffffffu;
             rs.order = h.order;
             rs.porder = h.porder;
-            /* a CONSTANT subframe has no residual: no partition headers to finish */
-            rs.nparts = (h.type == T_FIXED || h.type == T_LPC) ? 1u << h.porder : 0u;
+            rs.nparts = rice ? 1u << h.porder : 0u;
             rs.psamples = h.porder ? bs >> h.porder : bs - h.order;
             rs.plen = h.rice2 ? 5u : 4u;
             rs.pesc = h.rice2 ? 31u : 15u;
-            /* fused path: a chunk that lies inside one Rice partition (checked per chunk, so
-             * partitions need not be chunk-aligned: a chunk holding a partition boundary takes
-             * the generic path and the next one is fused again); the k_decode<8> instance
-             * leaves 64-bit-accumulator subframes to the generic path (keeps it at 128 VGPRs) */
-            fast_ok = (h.type == T_FIXED || (h.type == T_LPC && (MAXW > 8 || h.path != P_WIDE))) && !(ablate & 0x80Cu);
-            /* MMX path keeps raw warm-ups for output: stash them in the rows of chunk 0 */
-            if (h.type == T_LPC && h.path == P_MMX16) {
-                for (uint32_t t = 0; t < h.order; t++) row[t * RP] = warm[t];
-            }
         } else {
             active = false;
         }
@@ -1602,48 +1567,29 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : (MAXW == 16 ? 2 : 1
         const uint32_t n0 = kc * CHK;
         const uint32_t nvalid = (active && n0 < bs) ? min((uint32_t)CHK, bs - n0) : 0u;
         const uint64_t ta = tnow(tmon);
-        if (nvalid) {
-            /* full chunks past the warm-up take the fused path; partition headers and escaped
-             * partitions are handled inside it (rice_fused) */
-            const bool fast = fast_ok && nvalid == CHK && n0 >= h.order;
-            if (fast) {
-                STAT(b.stats, 0);
-                if (h.type == T_FIXED) fixed_fused<CHK>(b, rs, row, hh, h.order, h.wasted, limit, trunc);
-                else if (MAXW == 8 && h.path == P_MMX16) lpc_fused<CHK, 8, P_MMX16>(b, rs, row, c, hh, ht, sh, h.wasted, limit, trunc);
-                else if (MAXW == 8) lpc_fused<CHK, 8, P_IA32>(b, rs, row, c, hh, ht, sh, h.wasted, limit, trunc);
-                else LPC_DISPATCH(lpc_fused, b, rs, row, c, hh, ht, sh, h.wasted, limit, trunc);
+        br_wait1(b, vq); /* the lines fetched after the last entropy phase have landed */
+        /* full chunks past the warm-up: fused decode + restore; the warm-up chunk and a
+         * frame's last partial chunk: residuals into the rows, then the restore */
+        const bool fused = nvalid == CHK && n0 >= pd.order && !(ablate & 0x80Cu);
+        if (fused) {
+            STAT(b.stats, 0);
+            fused_chunk<CHK, MAXW>(b, rs, row, c, x, xt, pd, limit, trunc);
+        } else if (nvalid) {
+            STAT(b.stats, 1);
+            const uint32_t i0 = (n0 < pd.order) ? min(pd.order - n0, nvalid) : 0u;
+            if (ablate & 8u) {
+                for (uint32_t i = i0; i < nvalid; i++) row[i * RP] = (int32_t)i;
             } else {
-                STAT(b.stats, 1);
-                if (h.type == T_FIXED || h.type == T_LPC || h.type == T_VERB) {
-                    const uint32_t i0 = (n0 < h.order) ? h.order - n0 : 0u;
-                    if (ablate & 8u) {
-                        for (uint32_t i = i0; i < nvalid; i++) row[i * RP] = (int32_t)i;
-                    } else {
-                        for (uint32_t i = i0; i < nvalid; i++) row[i * RP] = next_val(b, rs, limit, trunc);
-                    }
-                }
-                if (ablate & 4u) {
-                    /* restore skipped (timing ablation) */
-                } else if (h.type == T_CONST) {
-                    for (uint32_t i = 0; i < nvalid; i++) row[i * RP] = (int32_t)((uint32_t)h.cval << h.wasted);
-                } else if (h.type == T_VERB) {
-                    for (uint32_t i = 0; i < nvalid; i++) row[i * RP] = (int32_t)((uint32_t)row[i * RP] << h.wasted);
-                } else if (h.type == T_FIXED) {
-                    fixed_chunk<CHK>(row, hh, n0, nvalid, h.order, h.wasted);
-                } else {
-                    LPC_DISPATCH(lpc_chunk, row, c, hh, ht, n0, nvalid, h.order, sh, h.wasted);
-                }
+                for (uint32_t i = i0; i < nvalid; i++) row[i * RP] = rice_fused(b, rs, limit, trunc, nullptr);
             }
         }
         const uint64_t tb = tnow(tmon);
-        /* stage the next chunk's blocks now: the wait inside finds the previous DMAs done.
-         * Since the previous refill this wave issued only the last pack's stores (CHK/8
-         * 16-byte stores on the stereo path): those keep draining in the background. */
-        {   /* whole wave: the vmcnt bookkeeping must stay uniform */
+        {   /* whole wave: fetch ahead while the restore and the pack run */
             const bool want = nvalid && h.type != T_CONST && n0 + CHK < bs;
             STAT(b.stats && want, 4);
-            br_refill2(b, want, vq, (ablate & 0x200u) != 0);
+            br_issue(b, want);
         }
+        if (!fused && nvalid && !(ablate & 4u)) restore_chunk<CHK, MAXW>(row, c, x, xt, pd, n0, nvalid);
         lds_sync();
         const uint64_t tc = tnow(tmon);
         tm_dec += tb - ta;
@@ -1779,7 +1725,7 @@ __global__ void __launch_bounds__(DEC_LANES, MAXW == 8 ? 3 : (MAXW == 16 ? 2 : 1
     }
     __syncthreads();
     if (tmon && lane == 0) {
-        const uint64_t t_end = __builtin_amdgcn_s_memtime();
+        const uint64_t t_end = tnow(tmon);
         atomicAdd(&g_stats[8], (unsigned long long)(t_loop - t_start));
         atomicAdd(&g_stats[9], (unsigned long long)tm_dec);
         atomicAdd(&g_stats[10], (unsigned long long)tm_ref);
@@ -2595,7 +2541,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
             lds_sync(); /* reads landed; the next chunk's staging writes come after them */
 #pragma unroll
             for (uint32_t r = 0; r < 4; r++) {
-                if (a[r]) *(u32x4 *)((uint8_t *)(uintptr_t)a[r] + 16u * fl_unit) = v[r];
+                if (a[r]) gst128(a[r] + 16u * fl_unit, v[r]);
                 if (any_lane(a[r] != 0)) nst += 1u;
             }
         }
@@ -2686,6 +2632,7 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
 #define TU_FN3(name, n) name##_tu##n
 #if BNF_TU == 1 || BNF_TU == 2 || BNF_TU == 5
 #define DEC_W (BNF_TU == 1 ? 8 : (BNF_TU == 5 ? 16 : 32))
+#define DEC_RD (BNF_TU == 2 ? 16 : 8) /* ring slots: LPC-32 subframes carry more bits per sample */
 extern "C" {
 hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     return upload_tables(crc8, crc16x8, xpow);
@@ -2707,7 +2654,7 @@ hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint
                                     hipStream_t s) {
     const uint32_t fpb = DEC_LANES / chn_lanes;
     const dim3 grid((nframes + fpb - 1) / fpb);
-    hipLaunchKernelGGL((k_decode<DEC_W, 32, 8>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt,
+    hipLaunchKernelGGL((k_decode<DEC_W, 32, DEC_RD>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt,
                        out, out_bytes, info, ablate_flags());
     return hipGetLastError();
 }
