@@ -53,10 +53,14 @@ CONFIGS = {
     "C2": dict(fmt="FLACDECODER", batches=1024, frames=1024,
                desc="C2: 1024-frame batches, 44.1 kHz/16-bit stereo, bs 4096, LPC-8, Rice partition order 4 "
                     "-> FLACDecoder 16-bit LE interleaved PCM"),
-    "C3": dict(fmt="FILEREADER", batches=64, frames=1024,
+    # C3/C4: 256 copies per step.  A C4 frame of 16384 samples is one lane's serial work, so
+    # at 32 copies the decode launch is as long as 1 copy (31.6 ms either way, r2 sweep):
+    # the step must hold enough frames to fill the chip (C4 256: 10.5 GB compressed, below
+    # the 16 GiB per-call limit)
+    "C3": dict(fmt="FILEREADER", batches=256, frames=1024,
                desc="C3: 1024-frame batches, 96 kHz/24-bit stereo, LPC-12, bs 8192, wasted bits + mid/side "
                     "-> FLACFileReader 24-bit LE interleaved PCM"),
-    "C4": dict(fmt="FLACDECODER", batches=32, frames=4096,
+    "C4": dict(fmt="FLACDECODER", batches=256, frames=4096,
                desc="C4: 4096-frame mixed corpus (CONSTANT/VERBATIM/FIXED/LPC, variable bs 192-16384), "
                     "16-bit stereo -> FLACDecoder 16-bit LE interleaved PCM"),
     "C5": dict(fmt="FILEREADER", batches=8, frames=469,

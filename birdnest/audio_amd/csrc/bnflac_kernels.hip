@@ -801,6 +801,7 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
         else sample = (uint64_t)fi.blocksize * fi.number;
         fi.out_sample = out_sample_in ? out_sample_in[f] : sample - base_sample;
         uint32_t maxorder = 0;
+        bool raw = false; /* a CONSTANT or VERBATIM subframe: k_decode_st would hand the frame back */
         for (uint32_t ch = 0; ch < fi.channels; ch++) {
             const uint32_t here = (uint32_t)(br_pos(b) - fbit);
 #pragma unroll
@@ -809,6 +810,7 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
                 /* the last subframe is walked by k_decode; only peek at its type byte */
                 const uint32_t x = br_peek(b) >> 24;
                 if (!(x & 0x80u) && (x & 0x7Eu) >= 0x40u) maxorder = max(maxorder, ((x >> 1) & 31u) + 1u);
+                raw = raw || (x & 0x7Eu) < 4u;
                 break;
             }
             if (ablate & 16u) {
@@ -822,6 +824,7 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
             st = parse_subframe_head<false>(b, bps, fi.blocksize, limit, h, nullptr, nullptr, err);
             if (st == BNF_ST_OK) {
                 if (h.type == T_LPC) maxorder = max(maxorder, h.order);
+                raw = raw || h.type == T_CONST || h.type == T_VERB;
                 if (h.type == T_VERB) br_skip(b, (uint64_t)h.bps * fi.blocksize);
                 else if (h.type == T_FIXED || h.type == T_LPC) st = skip_residual(b, h, fi.blocksize, limit, ablate);
                 if (st == BNF_ST_OK && br_pos(b) > limit) st = BNF_ST_TRUNC;
@@ -837,10 +840,10 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
         }
         /* decode instance: LPC orders above 16 -> k_decode<32>; 9..16, or LPC at more than 16
          * bits (libFLAC's 64-bit restore is then the usual path) -> k_decode<16>; 16-bit stereo
-         * otherwise -> k_decode_st; the rest -> k_decode<8> */
+         * with FIXED/LPC subframes only -> k_decode_st; the rest -> k_decode<8> */
         if (maxorder > 16) fi.flags |= BNF_FL_W32;
         else if (maxorder > 8 || (maxorder > 0 && fi.bps > 16)) fi.flags |= BNF_FL_W16;
-        else if (fi.channels == 2 && fi.bps <= 16) fi.flags |= BNF_FL_ST;
+        else if (fi.channels == 2 && fi.bps <= 16 && !raw) fi.flags |= BNF_FL_ST;
     }
     fi.status = st;
 #pragma unroll
@@ -1172,15 +1175,16 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
                                               uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate,
-                                              uint32_t nparse, uint32_t ncrc) {
+                                              uint32_t nparse, uint32_t ncrc, const uint32_t *__restrict__ perm) {
     __shared__ uint32_t ring[PARSE_RD * RING_LANE_DW]; /* parse: the bit ring; CRC: the tables */
     static_assert(PARSE_RD * RING_LANE_DW * 4 >= (8 * 256 + 512) * 2, "CRC tables fit the ring");
     const uint32_t lane = threadIdx.x;
     const uint32_t tot = nparse + ncrc, b = blockIdx.x;
     const uint32_t pb = (uint32_t)((uint64_t)b * nparse / tot), pb1 = (uint32_t)((uint64_t)(b + 1u) * nparse / tot);
     if (pb1 > pb) {
+        const uint32_t slot = pb * 64u + lane; /* parse order (launch_order<1>) */
         parse_frame(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
-                    pb * 64u + lane, ncrc != 0);
+                    (perm && slot < nframes) ? perm[slot] : slot, ncrc != 0);
         return;
     }
     lds_u16 *T = (lds_u16 *)(lds_u32 *)ring, *TK = T + 8 * 256;
@@ -1244,10 +1248,11 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
     const uint32_t bpsmp = (FMT == BNF_OUT_INTERLEAVED32) ? 8u : 4u;
     /* vector path (stereo): the frame's two lanes take interleaved 4-sample groups
      * (lane h: samples 8g+4h .. 8g+4h+3), so each 16-byte store instruction writes 32
-     * contiguous bytes per frame */
+     * contiguous bytes per frame; dword alignment is enough for a global dwordx4 store, so
+     * frames starting at any sample (variable blocksizes) take this path too */
     const uintptr_t base = (uintptr_t)out + (uintptr_t)(os + n0) * bpsmp;
     if ((FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_INTERLEAVED32) && C == 2 && chn_lanes == 2 && n0 + CH <= bs &&
-        (FMT == BNF_OUT_FLACDECODER || stream_channels == 2) && (base & 15u) == 0) {
+        (FMT == BNF_OUT_FLACDECODER || stream_channels == 2) && (base & 3u) == 0) {
         const int32_t *frows = lds + fl * 2u; /* (L, R) of sample i at frows[i * RP] */
 #pragma unroll
         for (int g = 0; g < CH / 8; g++) {
@@ -1395,7 +1400,8 @@ template <int MAXW, int CHK, int RD>
 __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
                                                       uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                       int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
-                                                      bnf_frame_info *__restrict__ info, uint32_t ablate) {
+                                                      bnf_frame_info *__restrict__ info,
+                                                      const uint32_t *__restrict__ perm, uint32_t ablate) {
     static_assert(MAXW <= CHK && CHK % 8 == 0 && RD <= RING_MAX, "chunk must hold the predictor ring");
     __shared__ uint32_t ring[RD * RING_LANE_DW];
     __shared__ int32_t lds[CHK * RP]; /* [sample][lane] */
@@ -1412,7 +1418,10 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
     const uint32_t lg = __builtin_ctz(chn_lanes); /* a power of 2 (lanes_for) */
     const uint32_t fpb = DEC_LANES >> lg;
     const uint32_t fl = lane >> lg, ch = lane & (chn_lanes - 1u);
-    const uint32_t f = blockIdx.x * fpb + fl;
+    /* frame of this lane group: slot order, or the decode order k_order built (class, then
+     * blocksize: similar frames share a wave) */
+    const uint32_t slot = blockIdx.x * fpb + fl;
+    const uint32_t f = (perm && fl < fpb && slot < nframes) ? perm[slot] : slot;
     const uint64_t limit = nbytes * 8u;
 
     bnf_frame_info fi;
@@ -1612,13 +1621,13 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
                                                     sp.bps == 24 ? 3u : 2u, out);
             break;
         }
-        /* account this chunk's stores for the next refill's counted vmcnt wait: the wave
-         * issued at least the store count of every lane that stored (a lower bound keeps
-         * the wait exact or conservative) */
+        /* account this chunk's stores for the next refill's counted vmcnt wait: every store
+         * of a lane is a store instruction of the wave, so the wave issued at least the
+         * largest per-lane count (a lower bound keeps the wait exact or conservative) */
         {
-            uint32_t m = pk ? pk : 0xFFFFFFFFu;
-            for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
-            vq.s_last += (m == 0xFFFFFFFFu) ? 0u : m;
+            uint32_t m = pk;
+            for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+            vq.s_last += m;
         }
         lds_sync();
         tm_pack += tnow(tmon) - tc;
@@ -2394,7 +2403,8 @@ template <int FMT>
 __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict__ words, uint64_t nbytes,
                                                      uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                      uint8_t *__restrict__ out, uint64_t out_bytes,
-                                                     bnf_frame_info *__restrict__ info, uint32_t ablate) {
+                                                     bnf_frame_info *__restrict__ info,
+                                                     const uint32_t *__restrict__ perm, uint32_t ablate) {
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t ST_SPG = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u; /* stores per 4 samples */
     __shared__ uint32_t ring[2 * ST_RD * RING_LANE_DW]; /* 16 KB: both channels' bitstream rings */
@@ -2404,7 +2414,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     if (ablate == 0xDEADu) occ_pad[threadIdx.x] = 1u;
 #endif
     const uint32_t lane = threadIdx.x;
-    const uint32_t f = blockIdx.x * 64u + lane;
+    const uint32_t slot = blockIdx.x * 64u + lane;
+    const uint32_t f = (perm && slot < nframes) ? perm[slot] : slot; /* decode order (k_order) */
     const uint64_t limit = nbytes * 8u;
     bnf_frame_info fi;
     const bool have = f < nframes;
@@ -2651,11 +2662,11 @@ hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
 }
 hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                     uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                                    hipStream_t s) {
+                                    const uint32_t *perm, hipStream_t s) {
     const uint32_t fpb = DEC_LANES / chn_lanes;
     const dim3 grid((nframes + fpb - 1) / fpb);
     hipLaunchKernelGGL((k_decode<DEC_W, 32, DEC_RD>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt,
-                       out, out_bytes, info, ablate_flags());
+                       out, out_bytes, info, perm, ablate_flags());
     return hipGetLastError();
 }
 } /* extern "C" */
@@ -2682,23 +2693,23 @@ hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
 /* stereo fast path; launched before k_decode<8> (it hands frames back to it) */
 hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                     uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                                    hipStream_t s) {
+                                    const uint32_t *perm, hipStream_t s) {
     const dim3 grid((nframes + 63) / 64);
     const uint32_t ab = ablate_flags();
     if (ab & 0x400u) return hipSuccess; /* timing ablation: everything to k_decode<8> */
 #if BNF_TU == 3
     (void)fmt;
-    hipLaunchKernelGGL(k_decode_st<BNF_OUT_FLACDECODER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, ab);
+    hipLaunchKernelGGL(k_decode_st<BNF_OUT_FLACDECODER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
 #else
     switch (fmt) {
     case BNF_OUT_PLANAR32:
-        hipLaunchKernelGGL(k_decode_st<BNF_OUT_PLANAR32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, ab);
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_PLANAR32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
         break;
     case BNF_OUT_INTERLEAVED32:
-        hipLaunchKernelGGL(k_decode_st<BNF_OUT_INTERLEAVED32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, ab);
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_INTERLEAVED32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
         break;
     default:
-        hipLaunchKernelGGL(k_decode_st<BNF_OUT_FILEREADER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, ab);
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_FILEREADER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
         break;
     }
 #endif
@@ -2716,14 +2727,14 @@ void bnf_set_ablate_tu4(uint32_t);
 hipError_t bnf_stats_tu3(uint64_t *, int);
 hipError_t bnf_stats_tu4(uint64_t *, int);
 hipError_t bnf_launch_decode_tu3(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
 hipError_t bnf_launch_decode_tu4(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
 hipError_t bnf_upload_tables_tu5(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu5(uint32_t);
 hipError_t bnf_stats_tu5(uint64_t *, int);
 hipError_t bnf_launch_decode_tu5(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
 hipError_t bnf_upload_tables_tu1(const uint8_t *, const uint16_t *, const uint16_t *);
 hipError_t bnf_upload_tables_tu2(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu1(uint32_t);
@@ -2731,9 +2742,9 @@ void bnf_set_ablate_tu2(uint32_t);
 hipError_t bnf_stats_tu1(uint64_t *, int);
 hipError_t bnf_stats_tu2(uint64_t *, int);
 hipError_t bnf_launch_decode_tu1(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
 hipError_t bnf_launch_decode_tu2(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
 
 hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     hipError_t e = upload_tables(crc8, crc16x8, xpow);
@@ -2781,26 +2792,132 @@ hipError_t bnf_stats(uint64_t *out16, int reset) {
 
 /* words: 16-byte aligned; the allocation must cover round_up(nbytes, 16) bytes. */
 /* crc: also run the coalesced CRC pass over [offset f, offset f+1) (info.crc_next) */
+} /* extern "C" */
+
+/* Frame orders: counting sorts that put similar frames into the same wave (lane- and
+ * wave-serial work is bounded by the longest frame of a wave).  Frames land in their bucket
+ * in any order: each frame's output and record depend on that frame only.
+ *  - decode order (MODE 0): decode class (k_parse's flags), then blocksize, descending;
+ *  - parse order (MODE 1): the subframe walk's length, blocksize x (channels - 1), read
+ *    from the frame header bytes (a heuristic: a bad header only lands in another bucket). */
+#define ORDER_NB 256
+DEV uint32_t order_bucket(uint32_t work) { return 63u - min(work >> 8, 63u); } /* larger first */
+template <int MODE>
+DEV uint32_t order_key(const bnf_frame_info *__restrict__ info, const uint8_t *__restrict__ bytes, uint64_t nbytes,
+                       const uint64_t *__restrict__ offs, uint32_t f) {
+    if (MODE == 0) {
+        const uint32_t st = info[f].status, fl = info[f].flags, bs = info[f].blocksize;
+        const uint32_t c = st != BNF_ST_OK ? 1u : (fl & BNF_FL_W32) ? 3u : (fl & BNF_FL_W16) ? 2u : (fl & BNF_FL_ST) ? 0u : 1u;
+        return c * 64u + order_bucket(bs ? bs - 1u : 0u);
+    }
+    const uint64_t o = offs[f];
+    if (o + 16u > nbytes) return 63u;
+    const uint32_t code = bytes[o + 2] >> 4, chc = bytes[o + 3] >> 4;
+    const uint32_t C = chc < 8u ? chc + 1u : 2u;
+    uint32_t bs = 0;
+    if (code == 1u) bs = 192u;
+    else if (code >= 2u && code <= 5u) bs = 576u << (code - 2u);
+    else if (code >= 8u) bs = 256u << (code - 8u);
+    else if (code == 6u || code == 7u) { /* 8 / 16 bits after the UTF-8 coded number */
+        const uint32_t lead = bytes[o + 4];
+        const uint32_t n = lead < 0x80u ? 1u : (uint32_t)__builtin_clz(~(lead << 24)); /* leading ones */
+        const uint64_t q = o + 4u + min(n, 7u);
+        bs = (code == 6u ? bytes[q] : ((uint32_t)bytes[q] << 8 | bytes[q + 1])) + 1u;
+    }
+    return order_bucket((bs * (C > 1u ? C - 1u : 1u)) >> 1);
+}
+template <int MODE>
+__global__ void __launch_bounds__(256) k_order_count(const bnf_frame_info *__restrict__ info,
+                                                     const uint8_t *__restrict__ bytes, uint64_t nbytes,
+                                                     const uint64_t *__restrict__ offs, uint32_t nframes,
+                                                     uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[ORDER_NB];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
+    if (f < nframes) atomicAdd(&h[order_key<MODE>(info, bytes, nbytes, offs, f)], 1u);
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+__global__ void __launch_bounds__(ORDER_NB) k_order_scan(uint32_t *__restrict__ hist) { /* exclusive, in place */
+    __shared__ uint32_t t[ORDER_NB];
+    const uint32_t i = threadIdx.x;
+    const uint32_t v = hist[i];
+    t[i] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < ORDER_NB; o <<= 1) {
+        const uint32_t a = i >= o ? t[i - o] : 0u;
+        __syncthreads();
+        t[i] += a;
+        __syncthreads();
+    }
+    hist[i] = t[i] - v;
+}
+template <int MODE>
+__global__ void __launch_bounds__(256) k_order_place(const bnf_frame_info *__restrict__ info,
+                                                     const uint8_t *__restrict__ bytes, uint64_t nbytes,
+                                                     const uint64_t *__restrict__ offs, uint32_t nframes,
+                                                     uint32_t *__restrict__ off, uint32_t *__restrict__ perm) {
+    __shared__ uint32_t h[ORDER_NB], base[ORDER_NB];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
+    uint32_t k = 0, r = 0;
+    if (f < nframes) {
+        k = order_key<MODE>(info, bytes, nbytes, offs, f);
+        r = atomicAdd(&h[k], 1u); /* rank within this block's share of the bucket */
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&off[threadIdx.x], h[threadIdx.x]);
+    __syncthreads();
+    if (f < nframes) perm[base[k] + r] = f;
+}
+/* order: ORDER_NB + nframes words of scratch; returns the permutation inside it */
+template <int MODE>
+static hipError_t launch_order(const bnf_frame_info *info, const uint8_t *bytes, uint64_t nbytes, const uint64_t *offs,
+                               uint32_t nframes, uint32_t *order, const uint32_t **perm, hipStream_t s) {
+    uint32_t *hist = order, *pm = order + ORDER_NB;
+    hipError_t e = hipMemsetAsync(hist, 0, ORDER_NB * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const dim3 g((nframes + 255) / 256);
+    hipLaunchKernelGGL(k_order_count<MODE>, g, dim3(256), 0, s, info, bytes, nbytes, offs, nframes, hist);
+    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(ORDER_NB), 0, s, hist);
+    hipLaunchKernelGGL(k_order_place<MODE>, g, dim3(256), 0, s, info, bytes, nbytes, offs, nframes, hist, pm);
+    *perm = pm;
+    return hipGetLastError();
+}
+
+extern "C" {
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
                             bnf_stream_params sp, const uint64_t *out_sample_in, uint64_t base_sample,
-                            bnf_frame_info *info, int crc, hipStream_t s) {
+                            bnf_frame_info *info, int crc, uint32_t *order, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
+    const uint32_t *perm = nullptr;
+    if (order) {
+        hipError_t e = launch_order<1>(nullptr, (const uint8_t *)words, nbytes, frame_offs, nframes, order, &perm, s);
+        if (e != hipSuccess) return e;
+    }
     const uint32_t np = (nframes + 63) / 64, nc = crc ? (nframes + CRC_FPW - 1) / CRC_FPW : 0u;
     hipLaunchKernelGGL(k_parse, dim3(np + nc), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
-                       out_sample_in, base_sample, info, ablate_flags(), np, nc);
+                       out_sample_in, base_sample, info, ablate_flags(), np, nc, perm);
     return hipGetLastError();
 }
 
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                              uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                             hipStream_t s) {
+                             uint32_t *order, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
+    const uint32_t *perm = nullptr;
+    if (order) {
+        hipError_t e = launch_order<0>(info, nullptr, 0, nullptr, nframes, order, &perm, s);
+        if (e != hipSuccess) return e;
+    }
     hipError_t e = fmt == BNF_OUT_FLACDECODER
-                       ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s)
-                       : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
-    if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
-    if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
-    if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, s);
+                       ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s)
+                       : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s);
     return e;
 }
 

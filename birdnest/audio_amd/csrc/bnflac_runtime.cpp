@@ -44,10 +44,11 @@ void bnf_set_ablate(uint32_t v);
 hipError_t bnf_stats(uint64_t *out16, int reset);
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs,
                             uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
-                            uint64_t base_sample, bnf_frame_info *info, int crc, hipStream_t s);
+                            uint64_t base_sample, bnf_frame_info *info, int crc, uint32_t *order, hipStream_t s);
+/* order: nullptr, or 256 + nframes words of device scratch for the frame order (k_order_*) */
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes,
                              bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
-                             bnf_frame_info *info, hipStream_t s);
+                             bnf_frame_info *info, uint32_t *order, hipStream_t s);
 hipError_t bnf_launch_chain(const uint8_t *bytes, uint64_t nbytes, const uint64_t *cand, uint32_t ncand,
                             const bnf_frame_info *info, uint64_t first_off, bnf_stream_params sp, uint32_t *gap_crc,
                             int32_t *jump, uint32_t levels, uint32_t *mark, uint32_t *pos, uint64_t *bs, uint8_t *small,
@@ -180,6 +181,7 @@ struct bnflac_ctx {
     uint32_t block_cap = 0;
     /* bnflac_index_stream scratch */
     CtxBuf cand, info, gap, jump, mark, pos, bs, small;
+    CtxBuf order, porder; /* decode / parse order: histogram + permutation (k_order_*) */
 };
 
 extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
@@ -194,7 +196,8 @@ extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
 extern "C" BNFLAC_API void bnflac_ctx_destroy(bnflac_ctx *ctx) {
     if (!ctx) return;
     if (ctx->d_block_counts) (void)hipFree(ctx->d_block_counts);
-    for (CtxBuf *b : {&ctx->cand, &ctx->info, &ctx->gap, &ctx->jump, &ctx->mark, &ctx->pos, &ctx->bs, &ctx->small})
+    for (CtxBuf *b : {&ctx->cand, &ctx->info, &ctx->gap, &ctx->jump, &ctx->mark, &ctx->pos, &ctx->bs, &ctx->small,
+                      &ctx->order, &ctx->porder})
         b->release();
     delete ctx;
 }
@@ -262,9 +265,11 @@ extern "C" BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_
     DevGuard dg(ctx->device); /* launches and scratch on the context's device */
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
+    if (!ctx->porder.grow(sizeof(uint32_t) * (256u + (size_t)nframes)))
+        return fail("bnflac_parse_frames: out of device memory (parse-order scratch)");
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, d_frame_offsets,
                                     nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info, crc_pass(),
-                                    (hipStream_t)hs);
+                                    (uint32_t *)ctx->porder.p, (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_parse: ") + hipGetErrorString(e));
 }
 
@@ -276,9 +281,11 @@ extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d
     if (out_format < 0 || out_format > 3) return fail("bnflac_decode_parsed: bad out_format");
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
+    if (!ctx->order.grow(sizeof(uint32_t) * (256u + (size_t)nframes)))
+        return fail("bnflac_decode_parsed: out of device memory (decode-order scratch)");
     hipError_t e = bnf_launch_decode((const uint32_t *)d_bytes, nbytes, nframes, p,
                                      lanes_for(sp->channels), out_format, d_out, out_bytes, (bnf_frame_info *)d_info,
-                                     (hipStream_t)hs);
+                                     (uint32_t *)ctx->order.p, (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_decode: ") + hipGetErrorString(e));
 }
 
@@ -326,7 +333,7 @@ extern "C" BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_
     memcpy(&p, sp, sizeof p);
     /* 2. header, CRC-8 and subframe walk of every candidate */
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, p, nullptr,
-                                    0, (bnf_frame_info *)ctx->info.p, 0, s);
+                                    0, (bnf_frame_info *)ctx->info.p, 0, nullptr, s);
     /* 3. successor chain, EOS rule, compaction */
     if (e == hipSuccess)
         e = bnf_launch_chain(d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, (const bnf_frame_info *)ctx->info.p,
@@ -755,7 +762,7 @@ bool decode_window(Dec *d, uint64_t base) {
             }
             if (!d->d_info.grow(sizeof(bnf_frame_info) * ncand)) goto oom;
             if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, n, (const uint64_t *)d->d_cand.p, ncand, sp,
-                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, 0, d->stream) != hipSuccess)
+                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, 0, nullptr, d->stream) != hipSuccess)
                 goto hip_fail;
             if (hipMemcpyAsync(d->info.data(), d->d_info.p, sizeof(bnf_frame_info) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
                 goto hip_fail;
@@ -777,7 +784,7 @@ bool decode_window(Dec *d, uint64_t base) {
             spd.channels = pcm_ch;
             if (bnf_launch_decode((const uint32_t *)d->d_bytes.p, n, ncand, spd, lanes_for(pcm_ch), BNF_OUT_PLANAR32,
                                   (uint8_t *)d->d_pcm.p, (uint64_t)std::max<uint64_t>(tot, 1) * pcm_ch * 4,
-                                  (bnf_frame_info *)d->d_info.p, d->stream) != hipSuccess)
+                                  (bnf_frame_info *)d->d_info.p, nullptr, d->stream) != hipSuccess)
                 goto hip_fail;
             d->pcm.resize((size_t)tot * pcm_ch);
             if (tot && hipMemcpyAsync(d->pcm.data(), d->d_pcm.p, sizeof(int32_t) * (size_t)tot * pcm_ch, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
