@@ -401,9 +401,27 @@ def reader_leg(wl, reps=3, chunk=16384):
         el = time.perf_counter() - t0
         ok = ok and got == wl.ref
         best = el if best is None else min(best, el)
-    return {"value": round(wl.samples1 / best / 1e6, 2), "unit": "MSamples/s", "ms": round(best * 1e3, 2),
-            "bitexact": bool(ok), "read_bytes": chunk,
-            "note": "host bytes -> bnflac_reader_open (H2D, index, decode-ahead) -> Read() x 16 KiB until EOS"}
+    out = {"value": round(wl.samples1 / best / 1e6, 2), "unit": "MSamples/s", "ms": round(best * 1e3, 2),
+           "bitexact": bool(ok), "read_bytes": chunk,
+           "note": "Python ctypes loop: host bytes -> bnflac_reader_open (H2D, index, one decode launch) -> "
+                   "Read() x 16 KiB until EOS"}
+    exe = os.path.join(ROOT, "tools", "reader_bench")
+    if os.path.exists(exe):  # the same pass driven from C (tools/reader_bench.c, built by build())
+        import subprocess
+        import tempfile
+        with tempfile.NamedTemporaryFile(suffix=".flac", delete=False) as tf:
+            tf.write(wl.data)
+        try:
+            r = subprocess.run([exe, tf.name, "10", str(chunk), str(wl.fmt)], capture_output=True, text=True,
+                               timeout=120)
+            if r.returncode == 0:
+                c = json.loads(r.stdout.strip().splitlines()[-1])
+                out["from_c"] = {"value": c["MSamples_per_s"], "ms": c["total_ms"], "open_ms": c["open_ms"],
+                                 "read_ms": c["read_ms"], "close_ms": c["close_ms"],
+                                 "note": "tools/reader_bench: best of 10 open + read x 16 KiB + close"}
+        finally:
+            os.unlink(tf.name)
+    return out
 
 
 def leg(cfg, args, torch, dev, libflac, synth, dec, stream):

@@ -6,11 +6,13 @@
  * `count` bytes of packed PCM at a time (4 x 16 KiB for OpenAL) and gets exactly the byte
  * sequence FLACDecoder.CopyTo would produce.
  *
- * On open the compressed stream goes to HBM once, bnflac_index_stream finds its frames,
- * and the decode then runs ahead of the reader in windows of frames: window w+1 is decoded
- * and copied into one slot of a pinned host ring while the caller drains window w from the
- * other.  Reads are memcpy from pinned memory; the GPU work and the D2H copies overlap
- * them.  A stream that is not intact (the frame chain ends before STREAMINFO's total, a
+ * On open the compressed stream goes to HBM once, bnflac_index_stream finds its frames and
+ * one bnflac_decode_parsed launch decodes all of them (a stream is far too small to fill the
+ * chip, so one launch costs what one window would).  The PCM then comes back in windows of
+ * frames: window w+1 is copied into one slot of a pinned host ring while the caller drains
+ * window w from the other.  Reads are memcpy from pinned memory; the D2H copies overlap
+ * them.  Device buffers, pinned slots, the stream and its events are kept in a per-device
+ * pool when a reader closes and reused by the next open (allocation dominated open/close).  A stream that is not intact (the frame chain ends before STREAMINFO's total, a
  * frame fails its CRC, or a frame needs the libFLAC error path) is refused at the point
  * it is reached, with bnflac_reader_last_error() saying why: the libFLAC stream API is the path
  * for damaged streams.
@@ -19,6 +21,10 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -46,6 +52,19 @@ int rfail(const std::string &m) {
 }
 
 /* STREAMINFO and the first frame offset from the metadata blocks (read_metadata_) */
+/* BNFLAC_READER_TRACE=1: open's phases to stderr (device-synchronised; development only) */
+struct OpenTrace {
+    bool on = getenv("BNFLAC_READER_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char *what, hipStream_t s) {
+        if (!on) return;
+        if (s) (void)hipStreamSynchronize(s);
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "reader_open %-14s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
 bool parse_metadata(const uint8_t *d, uint64_t n, bnflac_stream_params &sp, uint64_t &first) {
     if (n < 8 || memcmp(d, "fLaC", 4) != 0) return false;
     uint64_t p = 4;
@@ -117,6 +136,9 @@ struct bnflac_reader {
     bnflac_ctx *ctx = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
+    /* allocation sizes of the pooled buffers below (device: bytes, offs, os, info, out, n) */
+    size_t cap_bytes = 0, cap_offs = 0, cap_os = 0, cap_info = 0, cap_out = 0, cap_ring = 0, cap_hinfo = 0;
+    bnflac_frame_info *h_info = nullptr; /* pinned: every frame's record after the decode */
     bnflac_stream_params sp{};
     int fmt = BNFLAC_OUT_FLACDECODER;
     uint32_t stride = 0;
@@ -134,7 +156,6 @@ struct bnflac_reader {
     uint32_t cur = 0;                  /* window being read */
     uint64_t cur_pos = 0;              /* bytes of it already returned */
     uint64_t total_bytes = 0, returned = 0;
-    std::vector<bnflac_frame_info> winfo;
     bool failed = false;
     /* FLACFileReader compat mode (bnflac_reader_read_filereader): the C# reader's state */
     int mode = 0;                 /* 0 unused, 1 byte reads (bnflac_reader_read), 2 FLACFileReader reads */
@@ -153,20 +174,14 @@ uint64_t win_bytes(const bnflac_reader *r, uint32_t w) {
     return (r->os[f1] - r->os[f0]) * r->stride;
 }
 
-/* decode window w and copy it into its slot; asynchronous on r->stream */
+/* copy window w's PCM into its slot; asynchronous on r->stream (the decode of every frame
+ * was queued on it at open) */
 int issue_window(bnflac_reader *r, uint32_t w) {
     if (w >= r->nwin) return 0;
     const uint32_t slot = w & 1u;
-    const uint32_t f0 = w * r->window, nf = std::min(r->nframes, f0 + r->window) - f0;
-    bnflac_frame_info *info = (bnflac_frame_info *)r->d_info + f0;
-    if (bnflac_decode_parsed(r->ctx, (const uint8_t *)r->d_bytes, r->nbytes, nf, &r->sp, r->fmt, (uint8_t *)r->d_out,
-                             r->total_bytes, info, r->stream))
-        return rfail(std::string("bnflac_reader: ") + bnflac_last_error());
+    const uint32_t f0 = w * r->window;
     const uint64_t b0 = r->os[f0] * r->stride, nb = win_bytes(r, w);
     if (nb && hipMemcpyAsync(r->ring[slot], (const uint8_t *)r->d_out + b0, nb, hipMemcpyDeviceToHost, r->stream) != hipSuccess)
-        return rfail("bnflac_reader: D2H copy failed");
-    if (hipMemcpyAsync(r->winfo.data() + (size_t)slot * r->window, info, sizeof(bnflac_frame_info) * nf,
-                       hipMemcpyDeviceToHost, r->stream) != hipSuccess)
         return rfail("bnflac_reader: D2H copy failed");
     if (hipEventRecord(r->done[slot], r->stream) != hipSuccess) return rfail("bnflac_reader: event record failed");
     r->slot_win[slot] = w;
@@ -178,9 +193,9 @@ int land_window(bnflac_reader *r, uint32_t w) {
     const uint32_t slot = w & 1u;
     if (r->slot_win[slot] != w) return rfail("bnflac_reader: window not issued");
     if (hipEventSynchronize(r->done[slot]) != hipSuccess) return rfail("bnflac_reader: HIP error while decoding");
-    const uint32_t f0 = w * r->window, nf = std::min(r->nframes, f0 + r->window) - f0;
-    for (uint32_t i = 0; i < nf; i++) {
-        const bnflac_frame_info &fi = r->winfo[(size_t)slot * r->window + i];
+    const uint32_t f0 = w * r->window, f1 = std::min(r->nframes, f0 + r->window);
+    for (uint32_t i = f0; i < f1; i++) {
+        const bnflac_frame_info &fi = r->h_info[i];
         if (fi.status == 3 && (fi.flags & 4u))
             return rfail("bnflac_reader: frame at byte " + std::to_string(fi.frame_off) +
                          " cannot be carried by this output layout");
@@ -191,16 +206,84 @@ int land_window(bnflac_reader *r, uint32_t w) {
     return 0;
 }
 
-void release(bnflac_reader *r) {
-    if (r->stream) (void)hipStreamSynchronize(r->stream);
+/* per-device pool of one reader's resources (a closed reader's, for the next open) */
+std::mutex g_pool_mu;
+std::vector<bnflac_reader *> g_pool;
+
+void free_resources(bnflac_reader *r) {
     for (void *p : {r->d_bytes, r->d_offs, r->d_os, r->d_info, r->d_out, r->d_n})
         if (p) (void)hipFree(p);
     for (int i = 0; i < 2; i++) {
         if (r->ring[i]) (void)hipHostFree(r->ring[i]);
         if (r->done[i]) (void)hipEventDestroy(r->done[i]);
     }
+    if (r->h_info) (void)hipHostFree(r->h_info);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     if (r->ctx) bnflac_ctx_destroy(r->ctx);
+}
+
+/* a reader for `device`, with the pooled resources of an earlier one when there are any */
+bnflac_reader *take_reader(int device) {
+    bnflac_reader *r = new bnflac_reader();
+    r->device = device;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); i++) {
+        bnflac_reader *p = g_pool[i];
+        if (p->device != device) continue;
+        g_pool.erase(g_pool.begin() + (long)i);
+        r->ctx = p->ctx;
+        r->stream = p->stream;
+        r->d_bytes = p->d_bytes; r->cap_bytes = p->cap_bytes;
+        r->d_offs = p->d_offs; r->cap_offs = p->cap_offs;
+        r->d_os = p->d_os; r->cap_os = p->cap_os;
+        r->d_info = p->d_info; r->cap_info = p->cap_info;
+        r->d_out = p->d_out; r->cap_out = p->cap_out;
+        r->d_n = p->d_n;
+        r->ring[0] = p->ring[0]; r->ring[1] = p->ring[1]; r->cap_ring = p->cap_ring;
+        r->done[0] = p->done[0]; r->done[1] = p->done[1];
+        r->h_info = p->h_info; r->cap_hinfo = p->cap_hinfo;
+        delete p;
+        break;
+    }
+    return r;
+}
+
+bool dgrow(void *&p, size_t &cap, size_t n) { /* device buffer of at least n bytes */
+    if (p && cap >= n) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, n) != hipSuccess) return false;
+    cap = n;
+    return true;
+}
+template <typename T> bool hgrow(T *&p, size_t &cap, size_t n) { /* pinned host buffer */
+    if (p && cap >= n) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipHostMalloc((void **)&p, n, hipHostMallocDefault) != hipSuccess) return false;
+    cap = n;
+    return true;
+}
+
+/* close: the resources go back to the pool (one set per device) unless the reader failed
+ * in a way that may have left the stream in error */
+void release(bnflac_reader *r, bool keep = true) {
+    bool ok = !r->stream || hipStreamSynchronize(r->stream) == hipSuccess;
+    if (keep && ok && r->ctx && r->stream && r->done[0] && r->done[1]) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        bool have = false;
+        for (bnflac_reader *p : g_pool) have = have || p->device == r->device;
+        if (!have) {
+            bnflac_reader *p = new bnflac_reader();
+            *p = std::move(*r);
+            g_pool.push_back(p);
+            delete r;
+            return;
+        }
+    }
+    free_resources(r);
     delete r;
 }
 
@@ -218,75 +301,71 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
     if (out_format < 0 || out_format > 3) return rfail("bnflac_reader_open: bad out_format");
     if (device < 0 || device >= bnflac_device_count()) return rfail("bnflac_reader_open: bad device index");
     RDevGuard dg(device);
-    bnflac_reader *r = new bnflac_reader();
-    r->device = device;
+    OpenTrace tr;
+    bnflac_stream_params sp{};
+    uint64_t first = 0;
+    if (!parse_metadata(bytes, nbytes, sp, first))
+        return rfail("bnflac_reader_open: no fLaC marker / STREAMINFO (use the libFLAC stream API)");
+    if (sp.channels < 1 || sp.channels > 8) return rfail("bnflac_reader_open: bad channel count");
+    if (out_format == BNFLAC_OUT_FLACDECODER && sp.bps != 16) /* FLACDecoder.cs:526-529 aborts on these */
+        return rfail("bnflac_reader_open: FLACDecoder layout needs 16-bit samples, stream has " + std::to_string(sp.bps));
+    bnflac_reader *r = take_reader(device);
+    r->sp = sp;
     r->fmt = out_format;
     if (window_frames) r->window = window_frames;
-    uint64_t first = 0;
-    if (!parse_metadata(bytes, nbytes, r->sp, first)) {
-        release(r);
-        return rfail("bnflac_reader_open: no fLaC marker / STREAMINFO (use the libFLAC stream API)");
-    }
-    if (r->sp.channels < 1 || r->sp.channels > 8) {
-        release(r);
-        return rfail("bnflac_reader_open: bad channel count");
-    }
-    if (out_format == BNFLAC_OUT_FLACDECODER && r->sp.bps != 16) { /* FLACDecoder.cs:526-529 aborts on these */
-        release(r);
-        return rfail("bnflac_reader_open: FLACDecoder layout needs 16-bit samples, stream has " +
-                     std::to_string(r->sp.bps));
-    }
-    if (bnflac_ctx_create(device, &r->ctx)) {
+    if (!r->ctx && bnflac_ctx_create(device, &r->ctx)) {
         const std::string e = bnflac_last_error();
         r->ctx = nullptr;
-        release(r);
+        release(r, false);
         return rfail("bnflac_reader_open: " + e);
     }
     r->stride = bnflac_out_stride(out_format, &r->sp);
     r->nbytes = nbytes;
     const size_t padded = (size_t)((nbytes + 15) & ~15ull) + 16;
     const uint32_t cap = (uint32_t)std::min<uint64_t>(nbytes / 8 + 16, 1u << 30); /* a frame is >= 9 bytes */
-    if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&r->d_bytes, padded) != hipSuccess || hipMalloc(&r->d_offs, 8ull * cap) != hipSuccess ||
-        hipMalloc(&r->d_os, 8ull * cap) != hipSuccess || hipMalloc(&r->d_info, sizeof(bnflac_frame_info) * cap) != hipSuccess ||
-        hipMalloc(&r->d_n, 16) != hipSuccess) {
-        release(r);
+    size_t cap_n = 16;
+    if ((!r->stream && hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) ||
+        !dgrow(r->d_bytes, r->cap_bytes, padded) || !dgrow(r->d_offs, r->cap_offs, 8ull * cap) ||
+        !dgrow(r->d_os, r->cap_os, 8ull * cap) || !dgrow(r->d_info, r->cap_info, sizeof(bnflac_frame_info) * cap) ||
+        (!r->d_n && !dgrow(r->d_n, cap_n, 16)) ||
+        (!r->done[0] && hipEventCreateWithFlags(&r->done[0], hipEventDisableTiming) != hipSuccess) ||
+        (!r->done[1] && hipEventCreateWithFlags(&r->done[1], hipEventDisableTiming) != hipSuccess)) {
+        release(r, false);
         return rfail("bnflac_reader_open: out of device memory");
     }
+    tr.mark("ctx+alloc", r->stream);
     /* one H2D of the whole stream; the tail padding is zero */
     if (hipMemsetAsync((uint8_t *)r->d_bytes + (nbytes & ~15ull), 0, padded - (nbytes & ~15ull), r->stream) != hipSuccess ||
         hipMemcpyAsync(r->d_bytes, bytes, nbytes, hipMemcpyHostToDevice, r->stream) != hipSuccess) {
-        release(r);
+        release(r, false);
         return rfail("bnflac_reader_open: H2D copy failed");
     }
+    tr.mark("h2d", r->stream);
     if (bnflac_index_stream(r->ctx, (const uint8_t *)r->d_bytes, nbytes, first, &r->sp, (uint64_t *)r->d_offs,
                             (uint64_t *)r->d_os, (bnflac_frame_info *)r->d_info, cap, (uint32_t *)r->d_n, r->stream)) {
         const std::string e = bnflac_last_error();
-        release(r);
+        release(r, false);
         return rfail("bnflac_reader_open: " + e);
     }
     uint32_t nf = 0;
     if (hipMemcpyAsync(&nf, r->d_n, 4, hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
         hipStreamSynchronize(r->stream) != hipSuccess || nf > cap) {
-        release(r);
+        release(r, false);
         return rfail("bnflac_reader_open: frame index failed");
     }
+    tr.mark("index", r->stream);
     r->nframes = nf;
     r->os.resize((size_t)nf + 1);
-    if (nf && hipMemcpy(r->os.data(), r->d_os, 8ull * nf, hipMemcpyDeviceToHost) != hipSuccess) {
-        release(r);
+    /* the running sample counts, and the last frame's record (its blocksize ends the stream) */
+    bnflac_frame_info last{};
+    uint64_t last_off = 0;
+    if (nf && (hipMemcpy(r->os.data(), r->d_os, 8ull * nf, hipMemcpyDeviceToHost) != hipSuccess ||
+               hipMemcpy(&last, (bnflac_frame_info *)r->d_info + (nf - 1), sizeof last, hipMemcpyDeviceToHost) != hipSuccess ||
+               hipMemcpy(&last_off, (uint64_t *)r->d_offs + (nf - 1), 8, hipMemcpyDeviceToHost) != hipSuccess)) {
+        release(r, false);
         return rfail("bnflac_reader_open: D2H copy failed");
     }
-    /* the end of the last frame: its blocksize from its record */
-    uint64_t end = 0;
-    if (nf) {
-        bnflac_frame_info last;
-        if (hipMemcpy(&last, (bnflac_frame_info *)r->d_info + (nf - 1), sizeof last, hipMemcpyDeviceToHost) != hipSuccess) {
-            release(r);
-            return rfail("bnflac_reader_open: D2H copy failed");
-        }
-        end = r->os[nf - 1] + last.blocksize;
-    }
+    const uint64_t end = nf ? r->os[nf - 1] + last.blocksize : 0;
     r->os[nf] = end;
     if (r->sp.total_samples && end != r->sp.total_samples) {
         release(r);
@@ -297,13 +376,6 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
         /* length unknown (STREAMINFO total 0): a damaged frame would end the chain early with
          * every chained frame intact.  Refuse when an acceptable header numbered past the
          * chain's last frame follows it (trailing tags and metadata are allowed). */
-        uint64_t last_off = 0;
-        bnflac_frame_info last;
-        if (hipMemcpy(&last_off, (uint64_t *)r->d_offs + (nf - 1), 8, hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMemcpy(&last, (bnflac_frame_info *)r->d_info + (nf - 1), sizeof last, hipMemcpyDeviceToHost) != hipSuccess) {
-            release(r);
-            return rfail("bnflac_reader_open: D2H copy failed");
-        }
         const uint64_t last_no = last.number_type ? r->os[nf - 1] : last.number;
         for (uint64_t p = last_off + 2; p + 1 < nbytes; p++) {
             uint64_t no = 0;
@@ -320,23 +392,36 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
             }
         }
     }
+    tr.mark("index-readback", r->stream);
     r->total_bytes = end * r->stride;
     r->nwin = (nf + r->window - 1) / r->window;
-    for (uint32_t w = 0; w < r->nwin; w++) r->slot_bytes = std::max<size_t>(r->slot_bytes, win_bytes(r, w));
-    r->winfo.resize((size_t)2 * r->window);
-    if (hipMalloc(&r->d_out, std::max<uint64_t>(r->total_bytes, 16)) != hipSuccess ||
-        hipHostMalloc((void **)&r->ring[0], std::max<size_t>(r->slot_bytes, 16), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void **)&r->ring[1], std::max<size_t>(r->slot_bytes, 16), hipHostMallocDefault) != hipSuccess ||
-        hipEventCreateWithFlags(&r->done[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&r->done[1], hipEventDisableTiming) != hipSuccess) {
-        release(r);
+    size_t slot_bytes = 16;
+    for (uint32_t w = 0; w < r->nwin; w++) slot_bytes = std::max<size_t>(slot_bytes, win_bytes(r, w));
+    size_t c0 = r->cap_ring, c1 = r->cap_ring; /* the two slots are sized together */
+    if (!dgrow(r->d_out, r->cap_out, std::max<uint64_t>(r->total_bytes, 16)) || !hgrow(r->ring[0], c0, slot_bytes) ||
+        !hgrow(r->ring[1], c1, slot_bytes) ||
+        !hgrow(r->h_info, r->cap_hinfo, sizeof(bnflac_frame_info) * std::max(nf, 1u))) {
+        r->cap_ring = std::min(c0, c1);
+        release(r, false);
         return rfail("bnflac_reader_open: out of memory");
     }
-    /* decode-ahead: the first two windows */
+    r->cap_ring = std::min(c0, c1);
+    tr.mark("alloc-out", r->stream);
+    /* every frame in one decode launch, the records back to pinned memory, then the first
+     * two windows of PCM */
+    if (nf && (bnflac_decode_parsed(r->ctx, (const uint8_t *)r->d_bytes, r->nbytes, nf, &r->sp, r->fmt,
+                                    (uint8_t *)r->d_out, r->total_bytes, (bnflac_frame_info *)r->d_info, r->stream) ||
+               hipMemcpyAsync(r->h_info, r->d_info, sizeof(bnflac_frame_info) * nf, hipMemcpyDeviceToHost, r->stream) !=
+                   hipSuccess)) {
+        const std::string e = bnflac_last_error();
+        release(r, false);
+        return rfail("bnflac_reader_open: " + e);
+    }
     if (issue_window(r, 0) || issue_window(r, 1)) {
-        release(r);
+        release(r, false);
         return -1;
     }
+    tr.mark("decode+windows", r->stream);
     *out = r;
     return 0;
 }
@@ -440,7 +525,7 @@ int64_t fr_copy(bnflac_reader *r, uint8_t *buf, uint64_t len, uint64_t &noff) {
 
 /* FLACFileReader.Position / seek_absolute (FLACFileReader.cs:109-137,295-299): the next read
  * starts at sample `sample` (per channel).  The frame holding it is found in the index
- * (binary search over the running sample counts); its window and the next are decoded
+ * (binary search over the running sample counts); its window and the next are copied
  * again and the reader resumes inside the first. */
 BNFLAC_API int bnflac_reader_seek(bnflac_reader *r, uint64_t sample) {
     if (!r) return rfail("bnflac_reader_seek: null reader");
@@ -524,7 +609,7 @@ BNFLAC_API int64_t bnflac_reader_read_filereader(bnflac_reader *r, uint8_t *buff
 BNFLAC_API void bnflac_reader_close(bnflac_reader *r) {
     if (!r) return;
     RDevGuard dg(r->device);
-    release(r);
+    release(r, !r->failed);
 }
 
 } /* extern "C" */
