@@ -92,6 +92,11 @@ typedef __attribute__((address_space(1))) const void gvoid;
  * lgkmcnt -- every later LDS wait would then wait for the HBM write) */
 DEV void gst128(uint64_t addr, u32x4 v) { *(__attribute__((address_space(1))) u32x4 *)addr = v; }
 
+/* Mode bit carried in the kernels' `ablate` word (set by the launchers, never a timing
+ * ablation): the decode kernels leave the CRC-16 check to k_crc_join, because the
+ * concurrent CRC pass (k_crc, on a second stream) is still running. */
+#define BNF_MODE_DEFER_CRC 0x1000u
+
 /* ----------------------------------------------------------------- bit reader */
 #define RING_MAX 16       /* 16-byte slots per lane (k_parse and k_decode_st use 8) */
 #define RING_LANE_DW 256  /* dwords per slot row (64 lanes x 4) */
@@ -1175,7 +1180,8 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
                                               uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate,
-                                              uint32_t nparse, uint32_t ncrc, const uint32_t *__restrict__ perm) {
+                                              uint32_t nparse, uint32_t ncrc, const uint32_t *__restrict__ perm,
+                                              uint32_t keep_cn) {
     __shared__ uint32_t ring[PARSE_RD * RING_LANE_DW]; /* parse: the bit ring; CRC: the tables */
     static_assert(PARSE_RD * RING_LANE_DW * 4 >= (8 * 256 + 512) * 2, "CRC tables fit the ring");
     const uint32_t lane = threadIdx.x;
@@ -1184,7 +1190,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     if (pb1 > pb) {
         const uint32_t slot = pb * 64u + lane; /* parse order (launch_order<1>) */
         parse_frame(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
-                    (perm && slot < nframes) ? perm[slot] : slot, ncrc != 0);
+                    (perm && slot < nframes) ? perm[slot] : slot, ncrc != 0 || keep_cn != 0);
         return;
     }
     lds_u16 *T = (lds_u16 *)(lds_u32 *)ring, *TK = T + 8 * 256;
@@ -1197,6 +1203,67 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     const uint32_t lanec = crc16_shift(1u, 16u * (63u - lane));
     __syncthreads();
     crc_frames((const uint8_t *)words, nbytes, frame_offs, nframes, (b - pb) * CRC_FPW, info, T, TK, lanec, lane);
+}
+
+/* The same CRC pass as its own kernel, for a second stream: it runs beside k_parse and the
+ * decode kernels (it streams coalesced 1 KB loads; they are bound by lane-scattered memory
+ * requests), which then defer the check to k_crc_join. */
+__global__ void __launch_bounds__(64) k_crc(const uint32_t *__restrict__ words, uint64_t nbytes,
+                                            const uint64_t *__restrict__ frame_offs, uint32_t nframes,
+                                            bnf_frame_info *__restrict__ info) {
+    __shared__ uint32_t tabs[(8 * 256 + 512) / 2];
+    const uint32_t lane = threadIdx.x;
+    lds_u16 *T = (lds_u16 *)(lds_u32 *)tabs, *TK = T + 8 * 256;
+    for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
+    const uint32_t K = crc16_shift(1u, 1008u); /* x^(8*1008) mod P */
+    for (uint32_t i = lane; i < 256u; i += 64u) {
+        TK[i] = (uint16_t)gf_mul(i, K);
+        TK[256u + i] = (uint16_t)gf_mul(i << 8, K);
+    }
+    const uint32_t lanec = crc16_shift(1u, 16u * (63u - lane));
+    __syncthreads();
+    crc_frames((const uint8_t *)words, nbytes, frame_offs, nframes, blockIdx.x * CRC_FPW, info, T, TK, lanec, lane);
+}
+
+/* After the decode kernels and k_crc: the CRC-16 verdict of every deferred frame.  A frame
+ * whose footer ends where the next offset starts has its verdict in crc_next; any other
+ * (the last frame of a call, a gap before the next offset) is checked here, one thread per
+ * frame.  A mismatch zero-fills the frame's output, as libFLAC does (@0x10011af5) and as
+ * the decode kernels' own tail would have. */
+__global__ void __launch_bounds__(256) k_crc_join(const uint8_t *__restrict__ bytes, uint32_t nframes,
+                                                  bnf_stream_params sp, int fmt, uint8_t *__restrict__ out,
+                                                  bnf_frame_info *__restrict__ info) {
+    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
+    if (f >= nframes) return;
+    const uint32_t flags = info[f].flags;
+    if (info[f].status != BNF_ST_OK || !(flags & BNF_FL_CRC_DEFER)) return;
+    const uint64_t f_off = info[f].frame_off, end_byte = (info[f].resume_bit >> 3) - 2u; /* the footer's first byte */
+    const uint32_t rd = info[f].crc16_read, cn = info[f].crc_next;
+    uint32_t calc = rd;
+    if (!((cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && f_off + (cn & BNF_CN_LEN) == end_byte + 2u)) {
+        uint32_t c = 0;
+        for (uint64_t p = f_off; p < end_byte; p++) c = ((c << 8) ^ g_crc16_tab[0][((c >> 8) ^ bytes[p]) & 0xffu]) & 0xffffu;
+        calc = c;
+    }
+    info[f].crc16_calc = calc;
+    info[f].crc_ok = calc == rd ? 1u : 0u;
+    info[f].flags = flags & ~(uint32_t)BNF_FL_CRC_DEFER;
+    if (calc != rd) {
+        const uint32_t C = info[f].channels, bsz = info[f].blocksize;
+        const uint64_t os = info[f].out_sample;
+        uint64_t start, n;
+        switch (fmt) {
+        case BNF_OUT_PLANAR32: start = os * sp.channels * 4u; n = (uint64_t)C * bsz * 4u; break;
+        case BNF_OUT_INTERLEAVED32: start = os * sp.channels * 4u; n = (uint64_t)sp.channels * bsz * 4u; break;
+        case BNF_OUT_FLACDECODER: start = os * (C == 2 ? 4u : 2u); n = (uint64_t)bsz * (C == 2 ? 4u : 2u); break;
+        default: {
+            const uint32_t fb = sp.bps == 24 ? 3u : 2u;
+            start = os * sp.channels * fb;
+            n = (uint64_t)bsz * sp.channels * fb;
+        }
+        }
+        for (uint64_t i = 0; i < n; i++) out[start + i] = 0;
+    }
 }
 #endif
 
@@ -1684,10 +1751,15 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
                     t_crc_read = crc_read;
                     t_resume = br_pos(b);
                     t_resume_set = true;
-                    /* the k_parse launch's CRC pass found this frame's CRC-16 zero */
-                    const uint32_t cn = info[f].crc_next;
-                    if ((cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && f_off + (cn & BNF_CN_LEN) == end_byte + 2u)
+                    /* the k_parse launch's CRC pass found this frame's CRC-16 zero; or the
+                     * concurrent pass will be checked by k_crc_join */
+                    if (ablate & BNF_MODE_DEFER_CRC) {
                         t_pre[fl] = 1u;
+                    } else {
+                        const uint32_t cn = info[f].crc_next;
+                        if ((cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && f_off + (cn & BNF_CN_LEN) == end_byte + 2u)
+                            t_pre[fl] = 1u;
+                    }
                 }
             }
         }
@@ -1724,13 +1796,23 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
         fo.status = t_status;
         if (t_status == BNF_ST_ERROR) fo.err = t_err;
         if (t_resume_set) fo.resume_bit = t_resume;
-        if (t_status == BNF_ST_OK) {
+        if (t_status == BNF_ST_OK && (ablate & BNF_MODE_DEFER_CRC)) {
+            fo.crc16_read = t_crc_read;
+            fo.crc16_calc = 0;
+            fo.crc_ok = 0;
+            fo.flags |= BNF_FL_CRC_DEFER; /* k_crc_join decides (and zero-fills) */
+        } else if (t_status == BNF_ST_OK) {
             fo.crc16_read = t_crc_read;
             fo.crc16_calc = acc;
             fo.crc_ok = (acc == t_crc_read) ? 1u : 0u;
             if (!fo.crc_ok) t_bad[fl] = 2; /* libFLAC zero-fills a CRC-failed frame (@0x10011af5) */
         }
-        info[f] = fo;
+        { /* every word but crc_next, which the concurrent CRC pass may be writing */
+            const uint32_t *src = (const uint32_t *)&fo;
+            uint32_t *dst = (uint32_t *)&info[f];
+#pragma unroll
+            for (int i = 0; i < 31; i++) dst[i] = src[i];
+        }
     }
     __syncthreads();
     if (tmon && lane == 0) {
@@ -2586,7 +2668,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
      * of a batch, a gap before the next offset, a mismatch) the frame is re-read here. */
     uint32_t crc = crc_read;
     bool need = false;
-    if (ok) {
+    const bool defer = (ablate & BNF_MODE_DEFER_CRC) != 0; /* k_crc_join checks it */
+    if (ok && !defer) {
         const uint32_t cn = info[f].crc_next;
         const bool pre = (cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && fi.frame_off + (cn & BNF_CN_LEN) == end_byte + 2u;
         need = !pre && !(ablate & 1u);
@@ -2602,8 +2685,9 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     if (ok) {
         info[f].resume_bit = resume;
         info[f].crc16_read = crc_read;
-        info[f].crc16_calc = crc;
-        info[f].crc_ok = 1u;
+        info[f].crc16_calc = defer ? 0u : crc;
+        info[f].crc_ok = defer ? 0u : 1u;
+        if (defer) info[f].flags = fi.flags | BNF_FL_CRC_DEFER;
     } else if (mine) {
         info[f].flags = fi.flags | BNF_FL_REDO;
     }
@@ -2662,11 +2746,11 @@ hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
 }
 hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                     uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                                    const uint32_t *perm, hipStream_t s) {
+                                    const uint32_t *perm, uint32_t mode, hipStream_t s) {
     const uint32_t fpb = DEC_LANES / chn_lanes;
     const dim3 grid((nframes + fpb - 1) / fpb);
     hipLaunchKernelGGL((k_decode<DEC_W, 32, DEC_RD>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt,
-                       out, out_bytes, info, perm, ablate_flags());
+                       out, out_bytes, info, perm, ablate_flags() | mode);
     return hipGetLastError();
 }
 } /* extern "C" */
@@ -2693,9 +2777,9 @@ hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
 /* stereo fast path; launched before k_decode<8> (it hands frames back to it) */
 hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                     uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                                    const uint32_t *perm, hipStream_t s) {
+                                    const uint32_t *perm, uint32_t mode, hipStream_t s) {
     const dim3 grid((nframes + 63) / 64);
-    const uint32_t ab = ablate_flags();
+    const uint32_t ab = ablate_flags() | mode;
     if (ab & 0x400u) return hipSuccess; /* timing ablation: everything to k_decode<8> */
 #if BNF_TU == 3
     (void)fmt;
@@ -2727,14 +2811,14 @@ void bnf_set_ablate_tu4(uint32_t);
 hipError_t bnf_stats_tu3(uint64_t *, int);
 hipError_t bnf_stats_tu4(uint64_t *, int);
 hipError_t bnf_launch_decode_tu3(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_launch_decode_tu4(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_upload_tables_tu5(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu5(uint32_t);
 hipError_t bnf_stats_tu5(uint64_t *, int);
 hipError_t bnf_launch_decode_tu5(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_upload_tables_tu1(const uint8_t *, const uint16_t *, const uint16_t *);
 hipError_t bnf_upload_tables_tu2(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu1(uint32_t);
@@ -2742,9 +2826,9 @@ void bnf_set_ablate_tu2(uint32_t);
 hipError_t bnf_stats_tu1(uint64_t *, int);
 hipError_t bnf_stats_tu2(uint64_t *, int);
 hipError_t bnf_launch_decode_tu1(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_launch_decode_tu2(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
 
 hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     hipError_t e = upload_tables(crc8, crc16x8, xpow);
@@ -2888,36 +2972,57 @@ static hipError_t launch_order(const bnf_frame_info *info, const uint8_t *bytes,
 }
 
 extern "C" {
+/* crc: 0 none; 1 the CRC pass inside k_parse's launch; 2 k_crc on `side`, forked from s
+ * (ev_fork) and finished at ev_crc, for bnf_launch_decode's deferred check */
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
                             bnf_stream_params sp, const uint64_t *out_sample_in, uint64_t base_sample,
-                            bnf_frame_info *info, int crc, uint32_t *order, hipStream_t s) {
+                            bnf_frame_info *info, int crc, uint32_t *order, hipStream_t side, hipEvent_t ev_fork,
+                            hipEvent_t ev_crc, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
+    if (crc == 2) {
+        hipError_t e = hipEventRecord(ev_fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(side, ev_fork, 0);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_crc, dim3((nframes + CRC_FPW - 1) / CRC_FPW), dim3(64), 0, side, words, nbytes, frame_offs,
+                           nframes, info);
+        e = hipEventRecord(ev_crc, side);
+        if (e != hipSuccess) return e;
+    }
     const uint32_t *perm = nullptr;
     if (order) {
         hipError_t e = launch_order<1>(nullptr, (const uint8_t *)words, nbytes, frame_offs, nframes, order, &perm, s);
         if (e != hipSuccess) return e;
     }
-    const uint32_t np = (nframes + 63) / 64, nc = crc ? (nframes + CRC_FPW - 1) / CRC_FPW : 0u;
+    const uint32_t np = (nframes + 63) / 64, nc = crc == 1 ? (nframes + CRC_FPW - 1) / CRC_FPW : 0u;
     hipLaunchKernelGGL(k_parse, dim3(np + nc), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
-                       out_sample_in, base_sample, info, ablate_flags(), np, nc, perm);
+                       out_sample_in, base_sample, info, ablate_flags(), np, nc, perm, crc == 2 ? 1u : 0u);
     return hipGetLastError();
 }
 
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                              uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                             uint32_t *order, hipStream_t s) {
+                             uint32_t *order, hipEvent_t ev_crc, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
     const uint32_t *perm = nullptr;
     if (order) {
         hipError_t e = launch_order<0>(info, nullptr, 0, nullptr, nframes, order, &perm, s);
         if (e != hipSuccess) return e;
     }
+    const uint32_t mode = ev_crc ? BNF_MODE_DEFER_CRC : 0u; /* a concurrent CRC pass is running (k_crc) */
     hipError_t e = fmt == BNF_OUT_FLACDECODER
-                       ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s)
-                       : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s);
-    if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s);
-    if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s);
-    if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, s);
+                       ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s)
+                       : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    if (e == hipSuccess && ev_crc) {
+        e = hipStreamWaitEvent(s, ev_crc, 0);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_crc_join, dim3((nframes + 255) / 256), dim3(256), 0, s, (const uint8_t *)words, nframes,
+                               sp, fmt, out, info);
+            e = hipGetLastError();
+        }
+    }
     return e;
 }
 

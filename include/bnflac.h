@@ -177,9 +177,11 @@ BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uin
  * bit2 restore, bit3 Rice decode, bit4 subframe walk).  Output is wrong while set.
  * Exception: bit 0x800 only routes every k_decode chunk through the generic path (exact). */
 BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags);
-/* Mode switch (results stay exact): run the coalesced CRC-16 pass in bnflac_parse_frames'
- * launch (frame record crc_next) so the decode kernels skip their own CRC re-read for the
- * frames it vouches for.  Default off (env BNFLAC_CRC_PASS=1 turns it on). */
+/* Mode switch (results stay exact): run the coalesced CRC-16 pass (frame record crc_next)
+ * so the decode kernels skip their own CRC re-read for the frames it vouches for.
+ * 1: inside bnflac_parse_frames' launch; 2: on a second stream, concurrent with the parse
+ * and the decode of the same records (bnflac_decode_parsed then finishes the check).
+ * Default 0 (env BNFLAC_CRC_PASS=1|2). */
 BNFLAC_API void bnflac_debug_set_crc_pass(int on);
 /* Debug: k_decode event counters collected while ablate bit 0x100 is set: [0..5] fused
  * chunks, generic chunks, DMA landing waits, slow Rice codewords, refills, waves (wave-level

@@ -215,18 +215,43 @@ def test_crc_mismatch_zero_filled_in_batch(gpu):
                           np.delete(s.pcm, np.s_[2 * 4096: 3 * 4096], axis=0))
 
 
-def test_crc_pass_records_and_fallbacks(gpu):
-    """The coalesced CRC pass of the k_parse launch (frame record crc_next): valid and zero for
+@pytest.mark.parametrize("mode", [1, 2])
+def test_crc_pass_records_and_fallbacks(gpu, mode):
+    """The coalesced CRC pass (frame record crc_next), inside the k_parse launch (mode 1) or
+    as k_crc on a second stream with the verdict in k_crc_join (mode 2): valid and zero for
     intact frames followed by another offset, not zero for a corrupted frame, absent for the
     last frame; frames whose footer does not end at the next offset (junk in between) and the
-    last frame still get their CRC-16 checked by the decode kernels themselves."""
+    last frame still get their CRC-16 checked (decode kernels / k_crc_join)."""
     from birdnest.audio_amd import synth
     torch, libflac, _ = gpu
-    libflac.load().bnflac_debug_set_crc_pass(1)
+    libflac.load().bnflac_debug_set_crc_pass(mode)
     try:
         _crc_pass_cases(gpu, synth, libflac)
     finally:
         libflac.load().bnflac_debug_set_crc_pass(0)
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C5"])
+def test_crc_pass_modes_identical(gpu, cfg):
+    """Every CRC mode gives the same PCM and the same frame records (crc_next aside), with
+    no deferred-check flag left behind."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    s = synth.encode(synth.config(cfg, nframes={"C4": 96}.get(cfg, 24), last_blocksize=0))
+    res = []
+    for mode in (0, 1, 2):
+        libflac.load().bnflac_debug_set_crc_pass(mode)
+        try:
+            res.append(_decode_batch(gpu, s.data.tobytes(), s.frame_offsets, libflac.OUT_INTERLEAVED32))
+        finally:
+            libflac.load().bnflac_debug_set_crc_pass(0)
+    for out, info, _ in res[1:]:
+        assert out.tobytes() == res[0][0].tobytes()
+        for n in info.dtype.names:
+            if n != "crc_next":
+                assert np.array_equal(info[n], res[0][1][n]), n
+    assert not (res[2][1]["flags"] & 256).any()
+    assert (res[0][1]["crc_ok"] == 1).all()
 
 
 def _crc_pass_cases(gpu, synth, libflac):
