@@ -819,3 +819,41 @@ def test_empty_first_partition(gpu, order, bs, porder):
     ev, opcm = oracle.run(data)
     assert np.array_equal(pcm, oracle.interleave(ev, opcm))
     assert np.array_equal(pcm, s.pcm)
+
+
+def test_reader_pool_reuse_across_sizes_and_layouts(gpu):
+    """bnflac_reader_close keeps one reader's buffers per device and the next open reuses
+    them, growing what is too small: alternate small and large streams, both layouts, two
+    readers open at once (the second allocates afresh), a failed open in between."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    c2 = synth.encode(synth.config("C2", nframes=40, last_blocksize=0))
+    c2b = synth.encode(synth.config("C2", nframes=300, last_blocksize=1000, seed=77))
+    c3 = synth.encode(synth.config("C3", nframes=12))
+    want_c2 = c2.pcm.astype("<i2").tobytes()
+    want_c2b = c2b.pcm.astype("<i2").tobytes()
+    for _ in range(2):
+        for s, want in ((c2, want_c2), (c2b, want_c2b), (c2, want_c2)):
+            r = libflac.Reader(s.data.tobytes(), libflac.OUT_FLACDECODER, window_frames=16)
+            try:
+                assert r.read_all(16384) == want
+            finally:
+                r.close()
+        r = libflac.Reader(c3.data.tobytes(), libflac.OUT_FILEREADER, window_frames=4)
+        try:
+            got = r.read_all(49152)
+        finally:
+            r.close()
+        pcm = c3.pcm.astype("<i4")
+        ref = np.stack([(pcm >> 8 * k) & 0xFF for k in range(3)], axis=-1).astype(np.uint8).tobytes()
+        assert got == ref
+        with pytest.raises(RuntimeError):
+            libflac.Reader(b"not a flac stream", libflac.OUT_FLACDECODER)
+    a = libflac.Reader(c2b.data.tobytes(), libflac.OUT_FLACDECODER)
+    b = libflac.Reader(c2.data.tobytes(), libflac.OUT_FLACDECODER)
+    try:
+        assert b.read_all(1000) == want_c2
+        assert a.read_all(65536) == want_c2b
+    finally:
+        a.close()
+        b.close()
