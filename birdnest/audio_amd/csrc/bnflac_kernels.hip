@@ -1101,6 +1101,73 @@ DEV uint32_t crc16_shift(uint32_t crc, uint64_t nbytes) {
     return crc;
 }
 
+/* Wave-cooperative CRC-16 of one byte range (the whole wave, coalesced 1 KB loads).
+ * Layout: 16-byte pieces counted back from e = round_up(b1, 16); lane l takes pieces
+ * 63 - l + 64 m, so every wave load is 64 consecutive pieces.  Each lane runs a CRC over
+ * its own pieces with the 1008 bytes between them as zeros (x^(8*1008) by table TK), the
+ * result is shifted to e by lanec = x^(8*16*(63 - l)), and the lanes are XOR-reduced.
+ * Returns (wave-uniform) CRC([b0, b1)) * x^(8(e - b1)) mod P: zero iff the range's CRC is
+ * zero (x is invertible mod P).  Bytes outside
+ * [b0, b1) are masked to 0 (leading zeros leave a zero-initialised CRC at 0). */
+DEV uint32_t crc_mulk(uint32_t a, const lds_u16 *TK) { return TK[a & 0xffu] ^ TK[256u + (a >> 8)]; }
+DEV uint32_t byte_keep(int32_t lo, int32_t hi, int32_t w) { /* bytes 4w..4w+3 kept iff in [lo, hi) */
+    const int32_t a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
+    const uint32_t mlo = a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
+    const uint32_t mhi = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    return mlo & mhi;
+}
+DEV uint4 gld16(const uint8_t *p) { /* a global (not flat) 16-byte load */
+    const u32x4 v = *(__attribute__((address_space(1))) const u32x4 *)(uintptr_t)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+DEV uint32_t wave_crc_range(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T,
+                            const lds_u16 *TK, uint32_t lanec, uint32_t lane) {
+    const uint64_t e = (b1 + 15u) & ~15ull, a0 = b0 & ~15ull;
+    const uint32_t np = (uint32_t)((e - a0) >> 4), M = (np + 63u) >> 6;
+    uint32_t acc = 0;
+    for (uint32_t m0 = 0; m0 < M; m0 += 4u) {
+        uint4 v[4];
+        uint64_t pp[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t m = m0 + (uint32_t)u;
+            const uint32_t r = 63u - lane + 64u * (M - 1u - min(m, M - 1u));
+            pp[u] = e - 16ull * (r + 1u);
+            v[u] = (m < M && r < np) ? gld16(bytes + pp[u]) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (m0 + (uint32_t)u >= M) break; /* wave-uniform */
+            const int64_t lo = (int64_t)b0 - (int64_t)pp[u], hi = (int64_t)b1 - (int64_t)pp[u];
+            const bool edge = lo > 0 || hi < 16;
+            if (any_lane(edge)) {
+                if (edge) {
+                    const int32_t l32 = (int32_t)max(min(lo, (int64_t)16), (int64_t)0);
+                    const int32_t h32 = (int32_t)max(min(hi, (int64_t)16), (int64_t)0);
+                    v[u].x &= byte_keep(l32, h32, 0);
+                    v[u].y &= byte_keep(l32, h32, 1);
+                    v[u].z &= byte_keep(l32, h32, 2);
+                    v[u].w &= byte_keep(l32, h32, 3);
+                }
+            }
+            acc = crc_mulk(acc, TK);
+            acc = crc16_step8(acc, __builtin_bswap32(v[u].x), __builtin_bswap32(v[u].y), T);
+            acc = crc16_step8(acc, __builtin_bswap32(v[u].z), __builtin_bswap32(v[u].w), T);
+        }
+    }
+    acc = gf_mul(acc, lanec);
+    for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
+    return acc;
+}
+/* the TK table (x^(8*1008) by bytes) into LDS, by the whole wave */
+DEV void crc_tk_fill(lds_u16 *TK, uint32_t lane) {
+    const uint32_t K = crc16_shift(1u, 1008u);
+    for (uint32_t i = lane; i < 256u; i += 64u) {
+        TK[i] = (uint16_t)gf_mul(i, K);
+        TK[256u + i] = (uint16_t)gf_mul(i << 8, K);
+    }
+}
+
 #if BNF_TU == 0
 /* ============================================================== k_parse launch
  * One launch, two kinds of single-wave workgroups, interleaved by block index:
@@ -1118,14 +1185,6 @@ DEV uint32_t crc16_shift(uint32_t crc, uint64_t nbytes) {
  * outside [b0, b1) are masked to 0 (leading zeros leave a zero-initialised CRC at 0). */
 #define CRC_FPW 16
 
-DEV uint32_t crc_mulk(uint32_t a, const lds_u16 *TK) { return TK[a & 0xffu] ^ TK[256u + (a >> 8)]; }
-DEV uint32_t byte_keep(int32_t lo, int32_t hi, int32_t w) { /* bytes 4w..4w+3 kept iff in [lo, hi) */
-    const int32_t a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
-    const uint32_t mlo = a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
-    const uint32_t mhi = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
-    return mlo & mhi;
-}
-
 DEV void crc_frames(const uint8_t *__restrict__ bytes, uint64_t nbytes, const uint64_t *__restrict__ offs,
                     uint32_t nframes, uint32_t f0, bnf_frame_info *__restrict__ info, const lds_u16 *T,
                     const lds_u16 *TK, uint32_t lanec, uint32_t lane) {
@@ -1135,41 +1194,7 @@ DEV void crc_frames(const uint8_t *__restrict__ bytes, uint64_t nbytes, const ui
         const uint64_t b1 = f + 1u < nframes ? offs[f + 1u] : 0ull;
         uint32_t word = 0;
         if (b1 > b0 && b1 <= nbytes && b1 - b0 <= BNF_CN_LEN) { /* wave-uniform */
-            const uint64_t e = (b1 + 15u) & ~15ull, a0 = b0 & ~15ull;
-            const uint32_t np = (uint32_t)((e - a0) >> 4), M = (np + 63u) >> 6;
-            uint32_t acc = 0;
-            for (uint32_t m0 = 0; m0 < M; m0 += 4u) {
-                uint4 v[4];
-                uint64_t pp[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t m = m0 + (uint32_t)u;
-                    const uint32_t r = 63u - lane + 64u * (M - 1u - min(m, M - 1u));
-                    pp[u] = e - 16ull * (r + 1u);
-                    v[u] = (m < M && r < np) ? *(const uint4 *)(bytes + pp[u]) : make_uint4(0, 0, 0, 0);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    if (m0 + (uint32_t)u >= M) break; /* wave-uniform */
-                    const int64_t lo = (int64_t)b0 - (int64_t)pp[u], hi = (int64_t)b1 - (int64_t)pp[u];
-                    const bool edge = lo > 0 || hi < 16;
-                    if (any_lane(edge)) {
-                        if (edge) {
-                            const int32_t l32 = (int32_t)max(min(lo, (int64_t)16), (int64_t)0);
-                            const int32_t h32 = (int32_t)max(min(hi, (int64_t)16), (int64_t)0);
-                            v[u].x &= byte_keep(l32, h32, 0);
-                            v[u].y &= byte_keep(l32, h32, 1);
-                            v[u].z &= byte_keep(l32, h32, 2);
-                            v[u].w &= byte_keep(l32, h32, 3);
-                        }
-                    }
-                    acc = crc_mulk(acc, TK);
-                    acc = crc16_step8(acc, __builtin_bswap32(v[u].x), __builtin_bswap32(v[u].y), T);
-                    acc = crc16_step8(acc, __builtin_bswap32(v[u].z), __builtin_bswap32(v[u].w), T);
-                }
-            }
-            acc = gf_mul(acc, lanec);
-            for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
+            const uint32_t acc = wave_crc_range(bytes, b0, b1, T, TK, lanec, lane);
             word = BNF_CN_VALID | (acc == 0u ? BNF_CN_ZERO : 0u) | (uint32_t)(b1 - b0);
         }
         if (lane == 0) info[f].crc_next = word;
@@ -1195,11 +1220,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     }
     lds_u16 *T = (lds_u16 *)(lds_u32 *)ring, *TK = T + 8 * 256;
     for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
-    const uint32_t K = crc16_shift(1u, 1008u); /* x^(8*1008) mod P */
-    for (uint32_t i = lane; i < 256u; i += 64u) {
-        TK[i] = (uint16_t)gf_mul(i, K);
-        TK[256u + i] = (uint16_t)gf_mul(i << 8, K);
-    }
+    crc_tk_fill(TK, lane); /* x^(8*1008) mod P by bytes */
     const uint32_t lanec = crc16_shift(1u, 16u * (63u - lane));
     __syncthreads();
     crc_frames((const uint8_t *)words, nbytes, frame_offs, nframes, (b - pb) * CRC_FPW, info, T, TK, lanec, lane);
@@ -1215,11 +1236,7 @@ __global__ void __launch_bounds__(64) k_crc(const uint32_t *__restrict__ words, 
     const uint32_t lane = threadIdx.x;
     lds_u16 *T = (lds_u16 *)(lds_u32 *)tabs, *TK = T + 8 * 256;
     for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
-    const uint32_t K = crc16_shift(1u, 1008u); /* x^(8*1008) mod P */
-    for (uint32_t i = lane; i < 256u; i += 64u) {
-        TK[i] = (uint16_t)gf_mul(i, K);
-        TK[256u + i] = (uint16_t)gf_mul(i << 8, K);
-    }
+    crc_tk_fill(TK, lane); /* x^(8*1008) mod P by bytes */
     const uint32_t lanec = crc16_shift(1u, 16u * (63u - lane));
     __syncthreads();
     crc_frames((const uint8_t *)words, nbytes, frame_offs, nframes, blockIdx.x * CRC_FPW, info, T, TK, lanec, lane);
