@@ -257,7 +257,7 @@ def timed(wl, steps, warmup, stream, world, dist, dev):
 def roofline(alg_bytes, t_decode_ms, t_parse_ms, step_ms, traffic=None):
     achieved = alg_bytes / (t_decode_ms * 1e-3) / 1e9
     step = alg_bytes / (step_ms * 1e-3) / 1e9
-    r = {"bound": "hbm", "kernel": "decode launch (k_decode_st + k_decode<8> + k_decode<32>)",
+    r = {"bound": "hbm", "kernel": "decode launch (frame order + k_decode_st + k_decode<8|16|32>)",
          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
          "traffic": None, "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(t_decode_ms, 4),
          "k_parse_avg_ms": round(t_parse_ms, 4), "step_achieved_GBs": round(step, 1),
