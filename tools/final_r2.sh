@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-end measurement session (one gpurun call): every GPU test, a rocprofv3 kernel trace
+# + stats of each config's bench run, and the PMC passes (counters only, one rocprofv3 run
+# per pass) that tools/pmc_summary.py turns into profiles/traffic_<cfg>_b<B>.json.
+#   TAG=r2final bash tools/final_r2.sh        (outputs under gpurun_out/)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${TAG:-r2final}
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu \
+    > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/${TAG}_pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+for c in ${CFGS:-C2 C3 C4 C5}; do
+  TAG=$TAG CFG=$c STEPS=5 bash tools/prof_cfg.sh > gpurun_out/${TAG}_prof_$c.txt 2>&1 || { cat gpurun_out/${TAG}_prof_$c.txt; exit 1; }
+  head -8 gpurun_out/${TAG}_prof_$c.txt
+done
+for c in ${CFGS:-C2 C3 C4 C5}; do
+  PMC_BENCH_ARGS="--config $c --steps 2 --warmup 1 --legs= --no-cpu-baseline --no-pcie --no-index --no-reader" \
+  PMC_SETS='FETCH_SIZE
+WRITE_SIZE
+SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES' \
+  TAG=${TAG}_$c bash tools/pmc_session.sh || exit $?
+done
+echo "final session done"
