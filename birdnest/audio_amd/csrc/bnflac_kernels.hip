@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <mutex>
 
 #include "bnflac_device.h"
 
@@ -631,29 +632,40 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
              * the window shifted past the first (zeros shifted in can only make it not fit) */
             const uint32_t k1 = k + 1u, km = 31u - k;
             uint32_t rem = cnt;
+            /* the body is predicated (a lane whose partition is done advances 0 bits) rather
+             * than branched, and the refill counter is read as a scalar (the wave's lanes
+             * step together; it only paces refills), so an iteration carries no exec-mask
+             * bookkeeping beyond the loop test and the rare paths */
+            bool tr = false;
             while (any_lane(rem != 0u)) {
-                if (any_lane((since++ & 15u) == 0u) && !(ablate & 32u)) br_refill(b);
-                if (rem != 0u) {
-                    const uint32_t w = br_peek(b);
-                    const uint32_t q1 = ffbh(w); /* ~0u for an empty window */
-                    const bool fit1 = q1 <= km;
-                    const uint32_t len1 = q1 + k1;
-                    const uint32_t room = 32u - len1;
-                    const uint32_t q2 = ffbh(w << (len1 & 31u));
-                    const bool fit2 = fit1 && rem >= 2u && len1 < 32u && q2 < room && q2 + k1 <= room;
-                    const bool slow = any_lane(!fit1);
-                    br_adv(b, fit2 ? len1 + q2 + k1 : (fit1 ? len1 : 0u));
-                    rem -= fit2 ? 2u : (fit1 ? 1u : 0u);
-                    if (__builtin_expect(slow, 0)) {
-                        if (!fit1) {
-                            uint32_t qq;
-                            if (!br_unary(b, qq, limit)) return BNF_ST_TRUNC;
+                if ((__builtin_amdgcn_readfirstlane(since++) & 15u) == 0u && !(ablate & 32u)) br_refill(b);
+                const uint32_t m_live = 0u - (uint32_t)(rem != 0u);
+                const uint32_t w = br_peek(b);
+                const uint32_t q1 = ffbh(w); /* ~0u for an empty window */
+                const bool fit1 = q1 <= km;
+                const uint32_t len1 = q1 + k1;
+                const uint32_t room = 32u - len1;
+                const uint32_t q2 = ffbh(w << (len1 & 31u));
+                const bool fit2 = fit1 && rem >= 2u && len1 < 32u && q2 < room && q2 + k1 <= room;
+                const uint32_t a2 = len1 + q2 + k1, a1 = fit1 ? len1 : 0u;
+                const bool slow1 = m_live && !fit1;
+                const bool slow = any_lane(slow1);
+                br_adv(b, (fit2 ? a2 : a1) & m_live);
+                rem -= (fit2 ? 2u : (uint32_t)fit1) & m_live;
+                if (__builtin_expect(slow, 0)) {
+                    if (slow1) {
+                        uint32_t qq;
+                        if (br_unary(b, qq, limit)) {
                             br_adv(b, k);
                             rem--;
+                        } else { /* truncated: this lane stops walking */
+                            tr = true;
+                            rem = 0;
                         }
                     }
                 }
             }
+            if (tr) return BNF_ST_TRUNC;
         } else {
             const uint32_t k1 = k + 1u, km = 31u - k;
             for (uint32_t i = 0; i < cnt; i++) {
@@ -1511,15 +1523,26 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
     bnf_frame_info fi;
     bool have = (fl < fpb) && (f < nframes);
     if (have) fi = info[f];
-    /* stereo frames are k_decode_st's, unless it handed them back (BNF_FL_REDO) */
-    if (have && (fi.flags & BNF_FL_ST) && !(fi.flags & BNF_FL_REDO) && !(ablate & 0x400u)) have = false;
-    const bool frame_ok = have && fi.status == BNF_ST_OK;
+    /* Stereo frames (BNF_FL_ST) are k_decode_st's, unless it handed them back (BNF_FL_REDO):
+     * those are decoded by the W = 8 instance, which runs after k_decode_st on its stream.
+     * The W = 16 and 32 instances run beside them on a second stream and never look at
+     * ST frames (the ST bit is k_parse's and does not change; REDO may be being set). */
+    const bool st_frame = have && (fi.flags & BNF_FL_ST) && !(ablate & 0x400u);
+    if (st_frame && (MAXW != 8 || !(fi.flags & BNF_FL_REDO))) have = false;
+    bool frame_ok = have && fi.status == BNF_ST_OK;
     /* one wave per workgroup: the W = 8, 16 and 32 instances split the blocks between them
-     * by the widest class among the block's frames (k_parse's flags) */
+     * by the widest class among the block's non-ST frames (k_parse's flags); the W = 8
+     * instance also takes the handed-back ST frames of the other instances' blocks */
     {
-        const bool a32 = __any(frame_ok && (fi.flags & BNF_FL_W32)) != 0;
-        const bool a16 = __any(frame_ok && (fi.flags & BNF_FL_W16)) != 0;
-        if ((a32 ? 32 : (a16 ? 16 : 8)) != MAXW) return;
+        const bool a32 = __any(frame_ok && !st_frame && (fi.flags & BNF_FL_W32)) != 0;
+        const bool a16 = __any(frame_ok && !st_frame && (fi.flags & BNF_FL_W16)) != 0;
+        const int cls = a32 ? 32 : (a16 ? 16 : 8);
+        if (cls != MAXW) {
+            if (MAXW != 8) return;
+            have = have && st_frame; /* a W16/W32 block: only its handed-back ST frames */
+            frame_ok = frame_ok && st_frame;
+            if (!__any(have)) return;
+        }
     }
 
     bool active = frame_ok && ch < fi.channels && fi.channels <= chn_lanes;
@@ -2988,6 +3011,43 @@ static hipError_t launch_order(const bnf_frame_info *info, const uint8_t *bytes,
     return hipGetLastError();
 }
 
+/* The side stream of the current device for the W = 16 / 32 decode instances (created on
+ * first use, kept for the process), and the switch for the serial order
+ * (BNFLAC_DECODE_SERIAL=1: every decode instance on the caller's stream). */
+struct SideQ {
+    hipStream_t st;
+    hipEvent_t fork, join;
+};
+static std::mutex g_side_mu;
+static SideQ g_side[64];
+static bool decode_fork_enabled() {
+    static const int on = [] {
+        const char *e = getenv("BNFLAC_DECODE_SERIAL");
+        return (e && atoi(e) != 0) ? 0 : 1;
+    }();
+    return on != 0;
+}
+static SideQ *side_queue() { /* under g_side_mu; nullptr: decode serially */
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideQ &q = g_side[dev];
+    if (!q.st) {
+        hipStream_t st = nullptr;
+        hipEvent_t a = nullptr, b = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+            if (a) (void)hipEventDestroy(a);
+            (void)hipStreamDestroy(st);
+            return nullptr;
+        }
+        q.fork = a;
+        q.join = b;
+        q.st = st;
+    }
+    return &q;
+}
+
 extern "C" {
 /* crc: 0 none; 1 the CRC pass inside k_parse's launch; 2 k_crc on `side`, forked from s
  * (ev_fork) and finished at ev_crc, for bnf_launch_decode's deferred check */
@@ -3026,12 +3086,39 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         if (e != hipSuccess) return e;
     }
     const uint32_t mode = ev_crc ? BNF_MODE_DEFER_CRC : 0u; /* a concurrent CRC pass is running (k_crc) */
-    hipError_t e = fmt == BNF_OUT_FLACDECODER
-                       ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s)
-                       : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    /* k_decode_st -> k_decode<8> on s (k_decode<8> takes k_decode_st's hand-backs);
+     * k_decode<16> and k_decode<32> on the device's side stream, forked after the frame
+     * order and joined before anything that reads the whole batch.  The classes are disjoint
+     * frame sets and each instance alone rarely fills the chip (C4: 15.7 + 11.9 + 9.8 +
+     * 7.9 ms serialised).  The fork/join is enqueued under one lock, so concurrent callers
+     * sharing the side stream keep their own event pairs in order. */
+    std::unique_lock<std::mutex> lk(g_side_mu, std::defer_lock);
+    SideQ *sq = nullptr;
+    if (decode_fork_enabled()) {
+        lk.lock();
+        sq = side_queue();
+    }
+    hipError_t e = hipSuccess;
+    if (sq) {
+        e = hipEventRecord(sq->fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(sq->st, sq->fork, 0);
+        if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, sq->st);
+        if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, sq->st);
+        if (e == hipSuccess) e = hipEventRecord(sq->join, sq->st);
+        if (e != hipSuccess) return e;
+    }
+    e = fmt == BNF_OUT_FLACDECODER
+            ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s)
+            : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
     if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
-    if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
-    if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    if (sq) {
+        const hipError_t ej = hipStreamWaitEvent(s, sq->join, 0); /* joined even if a launch failed */
+        if (e == hipSuccess) e = ej;
+        lk.unlock();
+    } else {
+        if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+        if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    }
     if (e == hipSuccess && ev_crc) {
         e = hipStreamWaitEvent(s, ev_crc, 0);
         if (e == hipSuccess) {
