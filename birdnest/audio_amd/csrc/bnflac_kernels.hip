@@ -614,78 +614,86 @@ DEV uint32_t parse_subframe_head(BR &b, uint32_t bps, uint32_t bs, uint64_t limi
     return br_pos(b) > limit ? BNF_ST_TRUNC : BNF_ST_OK;
 }
 
-/* Skip the residual of a FIXED/LPC subframe (k_parse's cursor walk).  The ring is
- * refilled every 32 codewords (lanes of a wave stay in step on regular streams). */
+/* One step of k_parse's residual walk: up to two Rice codewords of the current partition
+ * (parameter k; km = 31 - k, k1 = k + 1).  Two codewords per 32-bit window when both fit:
+ * the second's prefix is counted in the window shifted past the first (zeros shifted in
+ * can only make it not fit).  Predicated: a lane with rem == 0 advances 0 bits. */
+DEV void skip_step(BR &b, uint32_t &rem, uint32_t k, uint32_t k1, uint32_t km, uint32_t &p, uint32_t parts, bool &tr,
+                   uint64_t limit) {
+    const uint32_t m_live = 0u - (uint32_t)(rem != 0u);
+    const uint32_t w = br_peek(b);
+    const uint32_t q1 = ffbh(w); /* ~0u for an empty window */
+    const bool fit1 = q1 <= km;
+    const uint32_t len1 = q1 + k1;
+    const uint32_t room = 32u - len1;
+    const uint32_t q2 = ffbh(w << (len1 & 31u));
+    const bool fit2 = fit1 && rem >= 2u && len1 < 32u && q2 < room && q2 + k1 <= room;
+    const uint32_t a2 = len1 + q2 + k1, a1 = fit1 ? len1 : 0u;
+    const bool slow1 = m_live && !fit1;
+    const bool slow = any_lane(slow1);
+    br_adv(b, (fit2 ? a2 : a1) & m_live);
+    rem -= (fit2 ? 2u : (uint32_t)fit1) & m_live;
+    if (__builtin_expect(slow, 0)) {
+        if (slow1) { /* a unary prefix too long for the window */
+            uint32_t qq;
+            if (br_unary(b, qq, limit)) {
+                br_adv(b, k);
+                rem--;
+            } else { /* truncated: this lane stops walking */
+                tr = true;
+                rem = 0;
+                p = parts;
+            }
+        }
+    }
+}
+
+/* Skip the residual of a FIXED/LPC subframe (k_parse's cursor walk).  One loop over the
+ * subframe's codewords: a lane whose partition is done reads the next partition header
+ * (and skips escaped partitions) on a rare path inside the same loop, so lanes whose
+ * partitions have different lengths (mixed partition orders in one wave) keep stepping
+ * together instead of waiting for the longest partition of every partition index.  The
+ * body is predicated (a lane with nothing left advances 0 bits), and the refill counter is
+ * read as a scalar (the wave's lanes step together; it only paces refills every 32
+ * codewords).  Returns BNF_ST_TRUNC when the walk runs past the buffer. */
 DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate) {
     const uint32_t parts = 1u << h.porder;
     const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
     const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
-    uint32_t since = 0;
-    for (uint32_t p = 0; p < parts; p++) {
-        const uint32_t k = br_read(b, plen);
-        const uint32_t cnt = (h.porder == 0 || p > 0) ? psamples : psamples - h.order;
-        if (k >= pesc) {
-            const uint32_t nb = br_read(b, 5);
-            br_skip(b, (uint64_t)nb * cnt);
-        } else if (!(ablate & 64u)) {
-            /* two codewords per 32-bit window when both fit: the second's prefix is counted in
-             * the window shifted past the first (zeros shifted in can only make it not fit) */
-            const uint32_t k1 = k + 1u, km = 31u - k;
-            uint32_t rem = cnt;
-            /* the body is predicated (a lane whose partition is done advances 0 bits) rather
-             * than branched, and the refill counter is read as a scalar (the wave's lanes
-             * step together; it only paces refills), so an iteration carries no exec-mask
-             * bookkeeping beyond the loop test and the rare paths */
-            bool tr = false;
-            while (any_lane(rem != 0u)) {
-                if ((__builtin_amdgcn_readfirstlane(since++) & 15u) == 0u && !(ablate & 32u)) br_refill(b);
-                const uint32_t m_live = 0u - (uint32_t)(rem != 0u);
-                const uint32_t w = br_peek(b);
-                const uint32_t q1 = ffbh(w); /* ~0u for an empty window */
-                const bool fit1 = q1 <= km;
-                const uint32_t len1 = q1 + k1;
-                const uint32_t room = 32u - len1;
-                const uint32_t q2 = ffbh(w << (len1 & 31u));
-                const bool fit2 = fit1 && rem >= 2u && len1 < 32u && q2 < room && q2 + k1 <= room;
-                const uint32_t a2 = len1 + q2 + k1, a1 = fit1 ? len1 : 0u;
-                const bool slow1 = m_live && !fit1;
-                const bool slow = any_lane(slow1);
-                br_adv(b, (fit2 ? a2 : a1) & m_live);
-                rem -= (fit2 ? 2u : (uint32_t)fit1) & m_live;
-                if (__builtin_expect(slow, 0)) {
-                    if (slow1) {
-                        uint32_t qq;
-                        if (br_unary(b, qq, limit)) {
-                            br_adv(b, k);
-                            rem--;
-                        } else { /* truncated: this lane stops walking */
-                            tr = true;
-                            rem = 0;
-                        }
+    uint32_t since = 0, p = 0, rem = 0, k = 0, k1 = 1, km = 31;
+    bool tr = false;
+    while (any_lane(rem != 0u || p < parts)) {
+        if ((__builtin_amdgcn_readfirstlane(since++) & 7u) == 0u && !(ablate & 32u)) br_refill(b);
+        const bool sw = rem == 0u && p < parts;
+        if (__builtin_expect(any_lane(sw), 0)) { /* partition headers (read_residual_partitioned_rice_ @0x10012da0) */
+            if (sw) {
+                do {
+                    if (br_pos(b) > limit) { /* the previous partition ended past the buffer */
+                        tr = true;
+                        p = parts;
+                        break;
                     }
-                }
-            }
-            if (tr) return BNF_ST_TRUNC;
-        } else {
-            const uint32_t k1 = k + 1u, km = 31u - k;
-            for (uint32_t i = 0; i < cnt; i++) {
-                if ((since++ & 31u) == 0 && !(ablate & 32u)) br_refill(b);
-                const uint32_t q = ffbh(br_peek(b)); /* ~0u for an empty window: slow */
-                const bool fast = q <= km;
-                const bool slow = any_lane(!fast);
-                br_adv(b, fast ? q + k1 : 0u);
-                if (__builtin_expect(slow, 0)) {
-                    if (!fast) {
-                        uint32_t qq;
-                        if (!br_unary(b, qq, limit)) return BNF_ST_TRUNC;
-                        br_adv(b, k);
+                    const uint32_t kk = br_read(b, plen);
+                    const uint32_t cnt = (h.porder == 0 || p > 0) ? psamples : psamples - h.order;
+                    p++;
+                    if (kk >= pesc) { /* escaped: cnt raw values of nb bits */
+                        const uint32_t nb = br_read(b, 5);
+                        br_skip(b, (uint64_t)nb * cnt);
+                    } else {
+                        k = kk;
+                        k1 = kk + 1u;
+                        km = 31u - kk;
+                        rem = cnt; /* 0: the empty first partition (order == partition size) */
                     }
-                }
+                } while (rem == 0u && p < parts);
             }
         }
-        if (br_pos(b) > limit) return BNF_ST_TRUNC;
+        /* two steps per switch test (a lane that finishes its partition in the first one
+         * idles in the second) */
+        skip_step(b, rem, k, k1, km, p, parts, tr, limit);
+        skip_step(b, rem, k, k1, km, p, parts, tr, limit);
     }
-    return BNF_ST_OK;
+    return (tr || br_pos(b) > limit) ? BNF_ST_TRUNC : BNF_ST_OK;
 }
 
 #if BNF_TU == 0
