@@ -1530,6 +1530,11 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
 
     bnf_frame_info fi;
     bool have = (fl < fpb) && (f < nframes);
+    if (MAXW != 8) { /* most blocks are not this instance's: leave on two words of the record */
+        const bool w = have && info[f].status == BNF_ST_OK && (info[f].flags & (BNF_FL_W16 | BNF_FL_W32)) &&
+                       !(info[f].flags & BNF_FL_ST);
+        if (!__any(w)) return;
+    }
     if (have) fi = info[f];
     /* Stereo frames (BNF_FL_ST) are k_decode_st's, unless it handed them back (BNF_FL_REDO):
      * those are decoded by the W = 8 instance, which runs after k_decode_st on its stream.
@@ -3019,39 +3024,43 @@ static hipError_t launch_order(const bnf_frame_info *info, const uint8_t *bytes,
     return hipGetLastError();
 }
 
-/* The side stream of the current device for the W = 16 / 32 decode instances (created on
- * first use, kept for the process), and the switch for the serial order
+/* The side streams of the current device for the W = 16 and W = 32 decode instances
+ * (created on first use, kept for the process), and the decode order
  * (BNFLAC_DECODE_SERIAL=1: every decode instance on the caller's stream). */
 struct SideQ {
-    hipStream_t st;
-    hipEvent_t fork, join;
+    hipStream_t st[2]; /* W16, W32 */
+    hipEvent_t fork, join[2];
 };
 static std::mutex g_side_mu;
 static SideQ g_side[64];
-static bool decode_fork_enabled() {
-    static const int on = [] {
+static int decode_fork_mode() { /* 0 serial; 1 fork after k_decode_st (default); 2 fork before it */
+    static const int m = [] {
         const char *e = getenv("BNFLAC_DECODE_SERIAL");
-        return (e && atoi(e) != 0) ? 0 : 1;
+        if (e && atoi(e) != 0) return 0;
+        const char *f = getenv("BNFLAC_DECODE_FORK");
+        return (f && atoi(f) == 2) ? 2 : 1;
     }();
-    return on != 0;
+    return m;
 }
 static SideQ *side_queue() { /* under g_side_mu; nullptr: decode serially */
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
     SideQ &q = g_side[dev];
-    if (!q.st) {
-        hipStream_t st = nullptr;
-        hipEvent_t a = nullptr, b = nullptr;
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
-            if (a) (void)hipEventDestroy(a);
-            (void)hipStreamDestroy(st);
+    if (!q.st[1]) {
+        SideQ n = {};
+        bool ok = hipEventCreateWithFlags(&n.fork, hipEventDisableTiming) == hipSuccess;
+        for (int i = 0; i < 2 && ok; i++)
+            ok = hipStreamCreateWithFlags(&n.st[i], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&n.join[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            for (int i = 0; i < 2; i++) {
+                if (n.join[i]) (void)hipEventDestroy(n.join[i]);
+                if (n.st[i]) (void)hipStreamDestroy(n.st[i]);
+            }
+            if (n.fork) (void)hipEventDestroy(n.fork);
             return nullptr;
         }
-        q.fork = a;
-        q.join = b;
-        q.st = st;
+        q = n;
     }
     return &q;
 }
@@ -3095,33 +3104,46 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
     }
     const uint32_t mode = ev_crc ? BNF_MODE_DEFER_CRC : 0u; /* a concurrent CRC pass is running (k_crc) */
     /* k_decode_st -> k_decode<8> on s (k_decode<8> takes k_decode_st's hand-backs);
-     * k_decode<16> and k_decode<32> on the device's side stream, forked after the frame
-     * order and joined before anything that reads the whole batch.  The classes are disjoint
-     * frame sets and each instance alone rarely fills the chip (C4: 15.7 + 11.9 + 9.8 +
-     * 7.9 ms serialised).  The fork/join is enqueued under one lock, so concurrent callers
-     * sharing the side stream keep their own event pairs in order. */
+     * k_decode<16> and k_decode<32> each on a side stream of the device, forked from s
+     * after k_decode_st and joined before anything that reads the whole batch: the classes
+     * are disjoint frame sets, and after k_decode_st (which fills the chip on its own) the
+     * three instances rarely do (C4: 15.7 + 9.8 + 7.9 ms serialised; 45 -> 41 ms).  Forking
+     * before k_decode_st (BNFLAC_DECODE_FORK=2) overlaps all four (C4 32 ms) but slows a
+     * batch with no W16/W32 frames (C2's k_decode_st +4%): the side launches' workgroups,
+     * early-exiting, still share the dispatcher and LDS slots with it; a high-priority
+     * stream for k_decode_st did not help.  The fork/join is enqueued under
+     * one lock, so concurrent callers sharing the side streams keep their event pairs in
+     * order. */
+    const int fm = decode_fork_mode();
     std::unique_lock<std::mutex> lk(g_side_mu, std::defer_lock);
     SideQ *sq = nullptr;
-    if (decode_fork_enabled()) {
+    if (fm) {
         lk.lock();
         sq = side_queue();
     }
     hipError_t e = hipSuccess;
-    if (sq) {
-        e = hipEventRecord(sq->fork, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(sq->st, sq->fork, 0);
-        if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, sq->st);
-        if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, sq->st);
-        if (e == hipSuccess) e = hipEventRecord(sq->join, sq->st);
-        if (e != hipSuccess) return e;
-    }
-    e = fmt == BNF_OUT_FLACDECODER
-            ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s)
-            : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    auto fork = [&]() -> hipError_t {
+        hipError_t r = hipEventRecord(sq->fork, s);
+        for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipStreamWaitEvent(sq->st[i], sq->fork, 0);
+        if (r == hipSuccess)
+            r = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, sq->st[1]);
+        if (r == hipSuccess)
+            r = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, sq->st[0]);
+        for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipEventRecord(sq->join[i], sq->st[i]);
+        return r;
+    };
+    if (sq && fm == 2) e = fork();
+    if (e == hipSuccess)
+        e = fmt == BNF_OUT_FLACDECODER
+                ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s)
+                : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    if (sq && fm == 1 && e == hipSuccess) e = fork();
     if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
     if (sq) {
-        const hipError_t ej = hipStreamWaitEvent(s, sq->join, 0); /* joined even if a launch failed */
-        if (e == hipSuccess) e = ej;
+        for (int i = 0; i < 2; i++) { /* joined even if a launch failed */
+            const hipError_t ej = hipStreamWaitEvent(s, sq->join[i], 0);
+            if (e == hipSuccess) e = ej;
+        }
         lk.unlock();
     } else {
         if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);

@@ -1,8 +1,9 @@
 """Decode-class split across streams (SURVEY.md 8a A10 dispatch; bnf_launch_decode).
 
-k_decode_st -> k_decode<8> run on the caller's stream and k_decode<16> / k_decode<32> on a
-side stream beside them.  k_decode<8> takes k_decode_st's hand-backs (BNF_FL_REDO) also in
-blocks that belong to the other instances, which never look at stereo fast-path frames.
+k_decode_st -> k_decode<8> run on the caller's stream, and k_decode<16> / k_decode<32> each
+on a side stream forked after k_decode_st (or before it, BNFLAC_DECODE_FORK=2).  k_decode<8>
+takes k_decode_st's hand-backs (BNF_FL_REDO) also in blocks that belong to the other
+instances, which never look at stereo fast-path frames.
 These tests put hand-back-prone stereo frames, LPC-12 (W16) and LPC-32 (W32) frames into
 one batch, so the decode order's 32-frame blocks mix the classes at their edges, and
 compare with the generator's source PCM and with the serial order (BNFLAC_DECODE_SERIAL=1,
@@ -88,10 +89,11 @@ sys.stdout.buffer.write(out.tobytes())
 
 
 @pytest.mark.skipif(not gpu_available(), reason="no GPU")
-def test_side_stream_matches_serial_order():
+@pytest.mark.parametrize("env", [{"BNFLAC_DECODE_SERIAL": "1"}, {"BNFLAC_DECODE_FORK": "2"}])
+def test_side_stream_matches_other_orders(env):
     data, offs, osmp, pcm, total = _mixed_batch(20)
     out, _ = _decode(data, offs, osmp, total)
-    env = dict(os.environ, BNFLAC_DECODE_SERIAL="1")
-    r = subprocess.run([sys.executable, "-c", _CHILD, ROOT], env=env, capture_output=True, timeout=100)
+    r = subprocess.run([sys.executable, "-c", _CHILD, ROOT], env=dict(os.environ, **env), capture_output=True,
+                       timeout=100)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     assert r.stdout == out.tobytes()
