@@ -22,4 +22,14 @@ WRITE_SIZE
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES' \
   TAG=${TAG}_$c bash tools/pmc_session.sh || exit $?
 done
+# PMC summaries (profiles/traffic_<cfg>_b<B>.json: bench.py's roofline.traffic for this build),
+# then the default bench line (every leg, CPU baselines) with them in place
+for cb in "C2 1024 1024" "C3 256 1024" "C4 256 4096" "C5 8 469"; do
+  set -- $cb
+  python3 tools/pmc_summary.py gpurun_out/pmc_${TAG}_$1 $1 $2 $3 $TAG > gpurun_out/traffic_${1,,}_b$2.json || exit 1
+  cp gpurun_out/traffic_${1,,}_b$2.json profiles/
+done
+timeout -k 10 900 python bench.py --out gpurun_out/${TAG}_bench.json > gpurun_out/${TAG}_bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -c 600 gpurun_out/${TAG}_bench.json
+[ $rc -eq 0 ] || exit $rc
 echo "final session done"
