@@ -999,12 +999,13 @@ struct Pred {
     bool mmx, wide;
 };
 
-/* the prediction of the sample at ring position T from the W history values */
-template <int T, int W>
+/* the prediction of the sample at ring position T from the W history values; only the
+ * first NT taps (the wave's coefficients past NT are all zero: NT covers its largest order) */
+template <int T, int W, int NT>
 DEV int32_t pred_at(const int32_t (&c)[W], const int32_t (&x)[W], const int32_t (&xt)[4], const Pred &p) {
     int64_t s0 = 0, s1 = 0;
 #pragma unroll
-    for (int t = 0; t < W; t++) {
+    for (int t = 0; t < NT; t++) {
         const int32_t hv = (t < 4) ? xt[(T - 1 - t) & 3] : x[((T - 1 - t) % W + W) % W];
         if (t & 1) s1 += (int64_t)c[t] * (int64_t)hv;
         else s0 += (int64_t)c[t] * (int64_t)hv;
@@ -1022,36 +1023,36 @@ DEV void push_at(int32_t (&x)[W], int32_t (&xt)[4], const Pred &p, int32_t s) {
 
 /* split path, samples T..W-1 of the W-sample group at row j (rows hold warm-ups /
  * residuals on entry, output samples on exit); n = subframe sample index of row j */
-template <int T, int W>
+template <int T, int W, int NT>
 DEV void restore_steps(int32_t *row, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4], const Pred &p,
                        uint32_t n, uint32_t nv, uint32_t j) {
     if constexpr (T < W) {
         const int32_t v = row[(j + T) * RP];
-        const int32_t pr = pred_at<T, W>(c, x, xt, p);
+        const int32_t pr = pred_at<T, W, NT>(c, x, xt, p);
         const int32_t s = (n + (uint32_t)T < p.order) ? v : (int32_t)((uint32_t)v + (uint32_t)pr);
         push_at<T, W>(x, xt, p, s);
         if (j + (uint32_t)T < nv) row[(j + T) * RP] = (int32_t)((uint32_t)s << p.wasted);
-        restore_steps<T + 1, W>(row, c, x, xt, p, n, nv, j);
+        restore_steps<T + 1, W, NT>(row, c, x, xt, p, n, nv, j);
     }
 }
 
 /* fused path (a full chunk past the warm-up): each residual goes from the bit reader
  * straight into the predictor, so the bit-cursor chain and the MAC chains of neighbouring
  * samples overlap; each row write is issued in the next codeword's cursor advance */
-template <int T, int W>
+template <int T, int W, int NT>
 DEV void fused_steps(BR &b, RS &rs, int32_t *row, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4],
                      const Pred &p, uint64_t limit, uint32_t &trunc, PendW &pw, uint32_t j) {
     if constexpr (T < W) {
         const int32_t r = rice_fused(b, rs, limit, trunc, &pw);
-        const int32_t s = (int32_t)((uint32_t)r + (uint32_t)pred_at<T, W>(c, x, xt, p));
+        const int32_t s = (int32_t)((uint32_t)r + (uint32_t)pred_at<T, W, NT>(c, x, xt, p));
         push_at<T, W>(x, xt, p, s);
         pw.v = (int32_t)((uint32_t)s << p.wasted);
         pw.at = row + (j + T) * RP;
         pw.on = true;
-        fused_steps<T + 1, W>(b, rs, row, c, x, xt, p, limit, trunc, pw, j);
+        fused_steps<T + 1, W, NT>(b, rs, row, c, x, xt, p, limit, trunc, pw, j);
     }
 }
-template <int CH, int W>
+template <int CH, int W, int NT>
 DEV void fused_chunk(BR &b, RS &rs, int32_t *row, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4],
                      const Pred &p, uint64_t limit, uint32_t &trunc) {
     PendW pw;
@@ -1059,16 +1060,16 @@ DEV void fused_chunk(BR &b, RS &rs, int32_t *row, const int32_t (&c)[W], int32_t
     pw.v = 0;
     pw.on = false;
 #pragma unroll 1
-    for (uint32_t j = 0; j < (uint32_t)CH; j += W) fused_steps<0, W>(b, rs, row, c, x, xt, p, limit, trunc, pw, j);
+    for (uint32_t j = 0; j < (uint32_t)CH; j += W) fused_steps<0, W, NT>(b, rs, row, c, x, xt, p, limit, trunc, pw, j);
     *pw.at = pw.v;
 }
 
 /* restore one chunk of CH rows (nv of them valid), W-sample groups */
-template <int CH, int W>
+template <int CH, int W, int NT>
 DEV void restore_chunk(int32_t *row, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4], const Pred &p,
                        uint32_t n0, uint32_t nv) {
 #pragma unroll 1
-    for (uint32_t j = 0; j < (uint32_t)CH; j += W) restore_steps<0, W>(row, c, x, xt, p, n0 + j, nv, j);
+    for (uint32_t j = 0; j < (uint32_t)CH; j += W) restore_steps<0, W, NT>(row, c, x, xt, p, n0 + j, nv, j);
 }
 
 /* CRC-16 (poly 0x8005) over bytes [b0, b1), slice-by-8 with the tables in LDS. */
@@ -1687,6 +1688,13 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
     uint32_t mybs = active ? bs : 0u;
     for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
     const uint32_t nchunks = (mybs + CHK - 1) / CHK;
+    /* W = 16 instance: a wave whose orders (taps with a nonzero coefficient: LPC and
+     * FIXED order, CONSTANT 1, VERBATIM 0) all fit NTAP_LO runs the predictor with NTAP_LO
+     * MACs per sample (C3's LPC-12 in k_decode<16>: 12 instead of 16) */
+    constexpr int NTAP_LO = MAXW * 3 / 4;
+    uint32_t mytaps = active ? pd.order : 0u;
+    for (int o = 32; o > 0; o >>= 1) mytaps = max(mytaps, (uint32_t)__shfl_xor(mytaps, o));
+    const bool ntap_lo = mytaps <= (uint32_t)NTAP_LO;
 
     const uint64_t t_loop = tnow(tmon);
     wait_vm(); /* setup loads done: the pipeline counts start from zero */
@@ -1702,7 +1710,8 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
         const bool fused = nvalid == CHK && n0 >= pd.order && !(ablate & 0x80Cu);
         if (fused) {
             STAT(b.stats, 0);
-            fused_chunk<CHK, MAXW>(b, rs, row, c, x, xt, pd, limit, trunc);
+            if (MAXW == 16 && ntap_lo) fused_chunk<CHK, MAXW, NTAP_LO>(b, rs, row, c, x, xt, pd, limit, trunc);
+            else fused_chunk<CHK, MAXW, MAXW>(b, rs, row, c, x, xt, pd, limit, trunc);
         } else if (nvalid) {
             STAT(b.stats, 1);
             const uint32_t i0 = (n0 < pd.order) ? min(pd.order - n0, nvalid) : 0u;
@@ -1718,7 +1727,10 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
             STAT(b.stats && want, 4);
             br_issue(b, want);
         }
-        if (!fused && nvalid && !(ablate & 4u)) restore_chunk<CHK, MAXW>(row, c, x, xt, pd, n0, nvalid);
+        if (!fused && nvalid && !(ablate & 4u)) {
+            if (MAXW == 16 && ntap_lo) restore_chunk<CHK, MAXW, NTAP_LO>(row, c, x, xt, pd, n0, nvalid);
+            else restore_chunk<CHK, MAXW, MAXW>(row, c, x, xt, pd, n0, nvalid);
+        }
         lds_sync();
         const uint64_t tc = tnow(tmon);
         tm_dec += tb - ta;
@@ -3114,7 +3126,10 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
      * stream for k_decode_st did not help.  The fork/join is enqueued under
      * one lock, so concurrent callers sharing the side streams keep their event pairs in
      * order. */
-    const int fm = decode_fork_mode();
+    /* Above 16 bits there are no stereo fast-path frames and LPC frames are W16/W32, so one
+     * instance does nearly all the work; forking would only add the other instances'
+     * early-exiting launches beside it (C3's k_decode<16>: 13.4 -> 15.0 ms) */
+    const int fm = sp.bps > 16 ? 0 : decode_fork_mode();
     std::unique_lock<std::mutex> lk(g_side_mu, std::defer_lock);
     SideQ *sq = nullptr;
     if (fm) {
