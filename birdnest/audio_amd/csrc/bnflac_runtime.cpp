@@ -439,6 +439,10 @@ struct FLAC__StreamDecoder {
     Md5 md5;
     uint64_t seek_target = 0;
     int seek_done = 0;
+    /* SEEKTABLE points (read_metadata_seektable_): sample number, byte offset from the first
+     * frame header, frame samples; placeholders dropped.  Only narrows a seek's search. */
+    struct SeekPoint { uint64_t sample, offset; uint32_t frame_samples; };
+    std::vector<SeekPoint> seek_table;
 
     FLAC__Frame frame;
     std::vector<int32_t> output[FLAC__MAX_CHANNELS];
@@ -646,6 +650,23 @@ bool read_metadata(Dec *d) {
         for (int i = 0; i < 16; i++) zero = zero && si.md5sum[i] == 0;
         if (zero) d->do_md5 = false;
         if (d->metadata_cb && !d->is_seeking) d->metadata_cb(d, &m, d->client);
+    } else if (type == FLAC__METADATA_TYPE_SEEKTABLE) {
+        /* read_metadata_seektable_: length / 18 points of (sample 64, offset 64, samples 16),
+         * kept whatever the respond set (libFLAC's seek uses them; no callback here, as the
+         * reference leaves metadata_respond at its STREAMINFO-only default) */
+        const uint64_t end = d->bitpos_meta + (uint64_t)length * 8;
+        d->seek_table.clear();
+        for (uint32_t i = 0; i < length / 18u; i++) {
+            uint32_t a, b, c, e, f;
+            if (!mb_read(d, &a, 32) || !mb_read(d, &b, 32) || !mb_read(d, &c, 32) || !mb_read(d, &e, 32) ||
+                !mb_read(d, &f, 16))
+                return false;
+            const uint64_t sample = ((uint64_t)a << 32) | b;
+            if (sample == ~0ull) continue; /* FLAC__STREAM_METADATA_SEEKPOINT_PLACEHOLDER */
+            d->seek_table.push_back({sample, ((uint64_t)c << 32) | e, f});
+        }
+        if (!need_bytes(d, end / 8)) return false;
+        d->bitpos_meta = end;
     } else {
         uint64_t end = d->bitpos_meta + (uint64_t)length * 8;
         if (!need_bytes(d, end / 8)) return false;
@@ -1003,6 +1024,7 @@ void reset_fields(Dec *d) {
     d->cached = false;
     d->client_done = 0;
     d->has_stream_info = false;
+    d->seek_table.clear();
     d->samples_decoded = 0;
     d->fixed_block_size = d->next_fixed_block_size = 0;
     d->first_frame_offset = 0;
@@ -1072,17 +1094,44 @@ bool window_at(Dec *d, uint64_t at, uint64_t bytes) {
  * bytes are still buffered; otherwise an interpolation search between known (offset,
  * sample) points, each probe one client seek + one GPU window (O(window) per probe,
  * O(log) probes), like libFLAC's seek_to_absolute_sample_ but over decoded windows. */
+bool seek_search(Dec *d, uint64_t target, uint64_t length, uint64_t *start, bool use_table);
+
 bool seek_position(Dec *d, uint64_t target, uint64_t length, uint64_t *start) {
     uint64_t off = 0, lo_off = d->first_frame_offset, lo_s = 0, hi_off = length, hi_s = 0;
     if (d->win_valid && window_find(d, target, &off, &lo_off, &lo_s, &hi_off, &hi_s) == 1 && off >= d->buf_base) {
         *start = off;
         return true;
     }
+    /* a SEEKTABLE only narrows the search; one that misleads it (offsets past the stream,
+     * points out of order) costs a second, table-free search, never different output */
+    if (!d->seek_table.empty() && seek_search(d, target, length, start, true)) return true;
+    return seek_search(d, target, length, start, false);
+}
+
+/* seek_to_absolute_sample_ over decoded windows; use_table: bracket the target between the
+ * SEEKTABLE points around it (libFLAC's lower/upper bound from the table) */
+bool seek_search(Dec *d, uint64_t target, uint64_t length, uint64_t *start, bool use_table) {
+    uint64_t off = 0, lo_off, lo_s, hi_off, hi_s;
     const FLAC__uint64 total = FLAC__stream_decoder_get_total_samples(d);
     lo_off = d->first_frame_offset;
     lo_s = 0;
     hi_off = length;
     hi_s = total ? total : ~0ull;
+    if (use_table) {
+        for (const auto &p : d->seek_table) {
+            if (p.frame_samples == 0 || (total && p.sample >= total)) continue;
+            const uint64_t o = d->first_frame_offset + p.offset;
+            if (p.offset > length || o >= length) continue;
+            if (p.sample <= target && p.sample >= lo_s && o >= lo_off) {
+                lo_s = p.sample;
+                lo_off = o;
+            } else if (p.sample > target && p.sample < hi_s && o < hi_off) {
+                hi_s = p.sample;
+                hi_off = o;
+            }
+        }
+        if (hi_off <= lo_off) return false;
+    }
     const uint32_t maxfs = d->has_stream_info ? d->stream_info.data.stream_info.max_framesize : 0;
     const uint64_t win = std::max<uint64_t>(1ull << 20, 4ull * (maxfs ? maxfs : 65536));
     for (int probe = 0; probe < 64; probe++) {

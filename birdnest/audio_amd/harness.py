@@ -79,6 +79,7 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
             return 1
         st["pos"] = int(off)
         st["eof"] = False
+        st["seek_calls"] = st.get("seek_calls", 0) + 1
         return 0
 
     def tl(d, off, ud):
@@ -156,6 +157,7 @@ def run(data: bytes, driver: int = 0, read_chunk: int = 16384, write_abort_at: i
         L.FLAC__stream_decoder_delete(dec)
     if stats is not None:
         stats["read_total"] = st.get("read_total", 0)
+        stats["seek_calls"] = st.get("seek_calls", 0)
     pcm = np.concatenate(pcm_parts) if pcm_parts else np.zeros(0, dtype=np.int32)
     if md5_check:
         return events, pcm, finish_ok

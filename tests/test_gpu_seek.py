@@ -101,3 +101,53 @@ def test_seek_refusals(gpu):
     data, s = _stream("C2", nframes=8)
     ev, pcm = _compare(gpu, data, [(2, 8 * 4096)])
     assert [e for e in ev if e[0] == gpu.EV_SEEK][0][1] == 0
+
+
+def _with_seektable(data, s, every, shift=0, placeholder=True):
+    """The stream with a SEEKTABLE block after STREAMINFO (libFLAC's layout: sample number,
+    byte offset from the first frame header, frame samples; 18 bytes a point, placeholders
+    0xFFFFFFFFFFFFFFFF last).  shift moves every offset (a misleading table)."""
+    bs = s.params.blocksize
+    first = int(s.frame_offsets[0])
+    pts = b""
+    n = 0
+    for i in range(0, len(s.frame_offsets), every):
+        off = int(s.frame_offsets[i]) - first + shift
+        pts += (i * bs).to_bytes(8, "big") + max(off, 0).to_bytes(8, "big") + bs.to_bytes(2, "big")
+        n += 1
+    if placeholder:
+        pts += b"\xff" * 8 + bytes(10)
+    assert data[:4] == b"fLaC" and data[4] & 0x7F == 0 and data[4] & 0x80  # STREAMINFO, last block
+    head = data[:4] + bytes([data[4] & 0x7F]) + data[5:42]
+    block = bytes([0x80 | 3]) + len(pts).to_bytes(3, "big") + pts
+    return head + block + data[42:]
+
+
+@pytest.mark.parametrize("cfg,kw,every,seeks", [
+    ("C2", dict(nframes=600), 16, [(-1, 517 * 4096 + 77), (3, 40 * 4096), (5, 599 * 4096 + 1)]),
+    ("C3", dict(nframes=60), 8, [(-1, 41 * 8192 + 5), (2, 7 * 8192)]),
+    ("C5", dict(nframes=40, last_blocksize=0), 4, [(1, 33 * 4096 + 100)]),
+])
+def test_seektable_narrows_seek_and_matches_oracle(gpu, cfg, kw, every, seeks):
+    """libFLAC reads a SEEKTABLE whatever the respond set (LibFLACSharp.cs:64 seek_absolute
+    uses it): the points bracket the search, so a seek takes fewer client seeks, and the
+    delivered callbacks and PCM are the oracle's, which ignores the table."""
+    plain, s = _stream(cfg, **kw)
+    data = _with_seektable(plain, s, every)
+    _compare(gpu, data, seeks)
+    st_tab, st_plain = {}, {}
+    ev_t, pcm_t = gpu.run(data, seeks=seeks, stats=st_tab)
+    ev_p, pcm_p = gpu.run(plain, seeks=seeks, stats=st_plain)
+    assert np.array_equal(pcm_t, pcm_p)
+    assert st_tab["seek_calls"] <= st_plain["seek_calls"], (st_tab, st_plain)
+    if cfg == "C2":  # a window from the bracketing point, not centred on an estimate: fewer bytes read
+        assert st_tab["read_total"] < st_plain["read_total"], (st_tab, st_plain)
+
+
+@pytest.mark.parametrize("shift", [-5000, 3, 1 << 40])
+def test_misleading_seektable_same_output(gpu, shift):
+    """A table whose offsets are wrong (before, inside or past the stream) costs a
+    table-free search, never different output."""
+    plain, s = _stream("C2", nframes=64)
+    data = _with_seektable(plain, s, 8, shift=shift)
+    _compare(gpu, data, [(-1, 50 * 4096 + 9), (2, 3 * 4096)])
