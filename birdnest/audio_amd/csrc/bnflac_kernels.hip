@@ -43,6 +43,12 @@
 __constant__ uint8_t g_crc8_tab[256];
 __constant__ uint16_t g_crc16_tab[8][256]; /* slice-by-8 */
 __constant__ uint16_t g_crc16_xpow[40];    /* x^(8*2^j) mod P for j < 40 */
+/* CRC-16 of an 8-byte block by six fields of 11/11/10 bits (crc16_step8w): the contribution
+ * of each field value to the block's CRC (init 0), fields at bit 53, 42, 32, 21, 10, 0 of the
+ * big-endian block; the last field's first 256 entries are the byte table.  20 KB. */
+#define CRC11_N 10240
+#define CRC11_BYTE 9216 /* offset of the last (10-bit) field's table = the byte table */
+__constant__ uint16_t g_crc16_t11[CRC11_N];
 
 /* Debug event counters (wave-level events, enabled by ablate bit 0x100; timing runs
  * leave them off).  0 fused chunks, 1 generic chunks, 2 DMA landing waits, 3 slow Rice
@@ -1079,6 +1085,12 @@ DEV uint32_t crc16_step8(uint32_t crc, uint32_t w0, uint32_t w1, const lds_u16 *
            T[4 * 256 + (a & 0xff)] ^ T[3 * 256 + (w1 >> 24)] ^ T[2 * 256 + ((w1 >> 16) & 0xff)] ^
            T[1 * 256 + ((w1 >> 8) & 0xff)] ^ T[w1 & 0xff];
 }
+/* the same 8-byte step with 6 lookups instead of 8 (tables: g_crc16_t11 in LDS) */
+DEV uint32_t crc16_step8w(uint32_t crc, uint32_t w0, uint32_t w1, const lds_u16 *T) {
+    const uint32_t a = w0 ^ (crc << 16);
+    return T[a >> 21] ^ T[2048 + ((a >> 10) & 0x7ffu)] ^ T[4096 + (a & 0x3ffu)] ^ T[5120 + (w1 >> 21)] ^
+           T[7168 + ((w1 >> 10) & 0x7ffu)] ^ T[CRC11_BYTE + (w1 & 0x3ffu)];
+}
 DEV uint32_t crc16_range(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
     uint32_t crc = 0;
     uint64_t p = b0;
@@ -2098,8 +2110,9 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  * @0x100118c0 and below) and the same PCM layouts (A15/A17), but:
  *   - the two channels' Rice + predictor chains interleave in one lane (ILP 2);
  *   - decorrelation (@0x10011a37-0x10011adb) and the PCM pack happen in registers, so
- *     there is no row buffer in LDS (LDS = the two bitstream rings, 8 KB per wave, and a
- *     4 KB tile that turns each frame's chunk of PCM into one 64-byte store run);
+ *     there is no row buffer in LDS (LDS = the two bitstream rings, 16 KB per wave); a
+ *     DPP transpose inside each lane quad turns each frame's chunk of PCM into one 64-byte
+ *     store run (16 frames per store instruction);
  *   - FIXED (@0x10003810), LPC MMX-16 and LPC ia32 restores share one predictor: four
  *     v_dot2_i32_i16 over the history kept as packed 16-bit sample pairs (the pmaddwd
  *     shape).  That is exact while every sample fits 16 bits (coefficients always do:
@@ -2370,32 +2383,57 @@ DEV void st_refill_issue(BR &b, bool want) {
     if (go) b.iend += 4u;
 }
 
-/* CRC-16 of [b0, b1) with two 64-byte loads in flight (tables in LDS) */
+/* CRC-16 of [b0, b1) with two 64-byte loads in flight (g_crc16_t11 tables in LDS: 0.75
+ * lookups per byte on whole lines, the byte table on the unaligned ends) */
+DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line offset o: bytes below h cleared */
+    return h <= o ? ~0u : (h >= o + 4u ? 0u : (~0u << (8u * (h - o))));
+}
 DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
+    const lds_u16 *Tb = T + CRC11_BYTE;
     uint32_t crc = 0;
+    /* whole lines from the one holding b0, its bytes below b0 taken as zeros (a CRC with
+     * init 0 stays 0 over leading zero bytes) */
+    const uint64_t p0 = b0 & ~(uint64_t)63u;
+    const uint32_t h = (uint32_t)(b0 & 63u);
+    const uint32_t nl = b1 > p0 ? (uint32_t)((b1 - p0) >> 6) : 0u;
     uint64_t p = b0;
-    while (p < b1 && (p & 63u)) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
-    const uint4 *q = (const uint4 *)(bytes + p);
-    const uint32_t nl = (uint32_t)((b1 - p) >> 6); /* whole 64-byte lines */
     if (nl) {
+        const uint4 *q = (const uint4 *)(bytes + p0);
         uint4 cur[4], nxt[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) cur[u] = q[u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            cur[u].x &= st_hmask(h, 16u * u);
+            cur[u].y &= st_hmask(h, 16u * u + 4u);
+            cur[u].z &= st_hmask(h, 16u * u + 8u);
+            cur[u].w &= st_hmask(h, 16u * u + 12u);
+        }
         for (uint32_t i = 0; i < nl; i++) {
             const uint32_t j = min(i + 1u, nl - 1u);
 #pragma unroll
             for (int u = 0; u < 4; u++) nxt[u] = q[4u * j + u];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                crc = crc16_step8(crc, __builtin_bswap32(cur[u].x), __builtin_bswap32(cur[u].y), T);
-                crc = crc16_step8(crc, __builtin_bswap32(cur[u].z), __builtin_bswap32(cur[u].w), T);
+                crc = crc16_step8w(crc, __builtin_bswap32(cur[u].x), __builtin_bswap32(cur[u].y), T);
+                crc = crc16_step8w(crc, __builtin_bswap32(cur[u].z), __builtin_bswap32(cur[u].w), T);
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) cur[u] = nxt[u];
         }
+        p = p0 + (uint64_t)nl * 64u;
+        /* the last partial line: whole 8-byte steps (loads issued together), then bytes */
+        const uint32_t n8 = (uint32_t)((b1 - p) >> 3);
+        const uint2 *q8 = (const uint2 *)(bytes + p);
+        uint2 t8[7];
+#pragma unroll
+        for (uint32_t i = 0; i < 7; i++) t8[i] = i < n8 ? q8[i] : make_uint2(0u, 0u);
+#pragma unroll
+        for (uint32_t i = 0; i < 7; i++)
+            if (i < n8) crc = crc16_step8w(crc, __builtin_bswap32(t8[i].x), __builtin_bswap32(t8[i].y), T);
+        p += 8u * n8;
     }
-    p += (uint64_t)nl * 64u;
-    while (p < b1) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
+    while (p < b1) { crc = ((crc << 8) ^ Tb[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
     return crc;
 }
 
@@ -2446,17 +2484,50 @@ DEV void st_rare(StCh &z, bool sl, bool ld, uint32_t &u, uint64_t limit, uint32_
     st_resync(z.b, lane);
 }
 
+/* 4x4 transpose of 16-byte units across the 4 lanes of each quad, in registers (DPP
+ * quad_perm, no LDS): on entry v[e] is unit e of this lane's frame, on exit v[i] is unit
+ * (lane & 3) of the frame of quad lane i.  Two exchange stages (lane bit 0 with unit bit 0,
+ * then bit 1): unit e is replaced by the partner's unit e ^ b where (lane ^ e) & b. */
+template <int CTRL>
+DEV uint32_t st_qperm(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true); }
+template <int CTRL, int B>
+DEV void st_quad_stage(u32x4 (&v)[4], bool pbit) {
+    u32x4 n[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const bool take = ((e & B) != 0) != pbit; /* (lane ^ e) & B */
+        const u32x4 o = v[e ^ B];
+        const u32x4 x = u32x4{st_qperm<CTRL>(o.x), st_qperm<CTRL>(o.y), st_qperm<CTRL>(o.z), st_qperm<CTRL>(o.w)};
+        n[e] = take ? x : v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++) v[e] = n[e];
+}
+DEV void st_quad_transpose(u32x4 (&v)[4], bool podd, bool phi) {
+    st_quad_stage<0xB1, 1>(v, podd); /* quad_perm [1,0,3,2] */
+    st_quad_stage<0x4E, 2>(v, phi);  /* quad_perm [2,3,0,1] */
+}
+/* quad lane i's 64-bit value (DPP quad_perm [i,i,i,i]) */
+DEV uint64_t st_quad_bcast64(uint64_t x, uint32_t i) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    switch (i) {
+    case 0: lo = st_qperm<0x00>(lo); hi = st_qperm<0x00>(hi); break;
+    case 1: lo = st_qperm<0x55>(lo); hi = st_qperm<0x55>(hi); break;
+    case 2: lo = st_qperm<0xAA>(lo); hi = st_qperm<0xAA>(hi); break;
+    default: lo = st_qperm<0xFF>(lo); hi = st_qperm<0xFF>(hi); break;
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
 /* One sample of both channels on the fused path (T: position in the 8-sample group).  The
  * two channels' predictor sums, Rice decodes and cursor advances form one basic block (a
  * single wave-uniform branch to the rare cases), so their dependency chains interleave.
- * STG: the 16-bit stereo layouts, whose packed words go to the LDS staging tile (stg: this
- * lane's 64-byte row, rotated by (lane >> 2) & 3 16-byte units: conflict-free both for the
- * per-lane b128 writes and for the frame-contiguous b128 reads of the flush); other layouts
- * store directly. */
+ * STG: the 16-bit stereo layouts, whose packed words stay in registers (pk: the group's two
+ * 16-byte units) until the chunk's flush (st_flush_quad); other layouts store directly. */
 template <int T, int FMT>
 DEV void st_fused_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
                        uint32_t nq, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al,
-                       uint32_t bs, bool store, lds_u32 *stg, uint32_t rot, uint32_t gq, int32_t &pre0, int32_t &pre1,
+                       uint32_t bs, bool store, u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1,
                        uint32_t lane, bool anyw) {
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t spg = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u;
@@ -2506,8 +2577,7 @@ DEV void st_fused_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
             uint32_t w[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_perm((uint32_t)R[q], (uint32_t)L[q], 0x05040100u);
-            const uint32_t u = (gq + (uint32_t)(T >> 2) + rot) & 3u; /* 16-byte unit in the row */
-            lds_st128((const void *)(stg + 4u * u), u32x4{w[0], w[1], w[2], w[3]});
+            pk[T >> 2] = u32x4{w[0], w[1], w[2], w[3]}; /* 16-byte unit 2g + (T >> 2) of the chunk's run */
         } else if (store) {
             st_emit4<FMT>(dst, nbase + (uint32_t)T - 3u, 4u, al, bs, L, R);
         }
@@ -2554,8 +2624,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ perm, uint32_t ablate) {
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t ST_SPG = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u; /* stores per 4 samples */
-    __shared__ uint32_t ring[2 * ST_RD * RING_LANE_DW]; /* 16 KB: both channels' bitstream rings */
-    __shared__ uint32_t stg_tile[64 * 16];              /* 4 KB: one 64-byte PCM run per frame */
+    /* 16 KB: both channels' bitstream rings; in the tail, the 20 KB CRC-16 field tables */
+    __shared__ uint32_t ring[(2 * ST_RD * RING_LANE_DW > CRC11_N / 2) ? 2 * ST_RD * RING_LANE_DW : CRC11_N / 2];
 #ifdef BNF_ST_PAD
     __shared__ uint32_t occ_pad[BNF_ST_PAD]; /* experiment: LDS padding to cap waves per CU */
     if (ablate == 0xDEADu) occ_pad[threadIdx.x] = 1u;
@@ -2606,10 +2676,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     const bool anyw = any_lane(ok && (z0.wasted | z1.wasted) != 0u);
     const uint32_t as_u = __builtin_amdgcn_readfirstlane(as);
     const bool as_uni = !any_lane(ok && as != as_u);
-    /* staging: this lane's row (write side), and the flush's frame / unit (read side) */
-    lds_u32 *stg_row = (lds_u32 *)stg_tile + lane * 16u;
-    const uint32_t rot = (lane >> 2) & 3u;
-    const uint32_t fl_unit = lane & 3u;
+    const uint32_t fl_unit = lane & 3u; /* the flush: this lane's 16-byte unit of a frame's 64-byte run */
+    const bool podd = (lane & 1u) != 0, phi = (lane & 2u) != 0;
 
     uint32_t mybs = ok ? bs : 0u;
     for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
@@ -2629,6 +2697,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
             fast = !z0.esc && !z1.esc && z0.left >= ST_CHK && z1.left >= ST_CHK;
         }
         const bool fused = !any_lane(valid && !fast);
+        u32x4 pk[2], pk01[2]; /* the chunk's four 16-byte units (STG): pk01 from g = 0, pk from g = 1 */
         if (fused) {
             if (valid) {
                 STAT(z0.b.stats, 0);
@@ -2642,9 +2711,10 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                     const uint32_t nq = nst + (STG ? 0u : g * 2u * ST_SPG); /* stores issued since the DMAs (at least) */
                     const uint32_t nb = n0 + g * 8u;
                     const bool sto = !(ablate & 2u);
-#define FSTEP(T) st_fused_step<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, stg_row, rot, 2u * g, pre0, pre1, lane, anyw)
+#define FSTEP(T) st_fused_step<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
                     FSTEP(0); FSTEP(1); FSTEP(2); FSTEP(3); FSTEP(4); FSTEP(5); FSTEP(6); FSTEP(7);
 #undef FSTEP
+                    if (STG && g == 0) { pk01[0] = pk[0]; pk01[1] = pk[1]; }
                 }
                 z0.left -= ST_CHK;
                 z1.left -= ST_CHK;
@@ -2686,21 +2756,13 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         tm_ref += tc - tb;
         if (STG && fused) { /* flush: 4 lanes per frame, one 64-byte run each, 16 frames per store */
             const uint64_t run = (valid && !(ablate & 2u)) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull;
-            lds_sync();
-            uint64_t a[4];
-            u32x4 v[4];
+            u32x4 v[4] = {pk01[0], pk01[1], pk[0], pk[1]};
+            st_quad_transpose(v, podd, phi); /* v[i]: unit (lane & 3) of the quad's frame i */
 #pragma unroll
-            for (uint32_t r = 0; r < 4; r++) {
-                const uint32_t fr = 16u * r + (lane >> 2);
-                a[r] = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(run >> 32), (int)fr) << 32) |
-                       (uint32_t)__shfl((int)(uint32_t)run, (int)fr);
-                v[r] = lds_ld128((const void *)((lds_u32 *)stg_tile + fr * 16u + 4u * ((fl_unit + (fr >> 2)) & 3u)));
-            }
-            lds_sync(); /* reads landed; the next chunk's staging writes come after them */
-#pragma unroll
-            for (uint32_t r = 0; r < 4; r++) {
-                if (a[r]) gst128(a[r] + 16u * fl_unit, v[r]);
-                if (any_lane(a[r] != 0)) nst += 1u;
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint64_t a = st_quad_bcast64(run, i);
+                if (a) gst128(a + 16u * fl_unit, v[i]);
+                if (any_lane(a != 0)) nst += 1u;
             }
         }
         tm_pack += tnow(tmon) - tc;
@@ -2742,7 +2804,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     if (any_lane(need)) {
         wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
         lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
-        for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
+        for (uint32_t i = lane; i < CRC11_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
         __syncthreads();
         if (need) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
     }
@@ -2784,6 +2846,20 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
     if (e != hipSuccess) return e;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_tab), crc16x8, 8 * 256 * sizeof(uint16_t));
     if (e != hipSuccess) return e;
+    { /* field tables from the byte table (crc16x8[0]): CRC of the 8-byte block v << shift */
+        static const uint32_t sh[6] = {53, 42, 32, 21, 10, 0}, wd[6] = {11, 11, 10, 11, 11, 10};
+        uint16_t t11[CRC11_N];
+        uint32_t at = 0;
+        for (int fld = 0; fld < 6; fld++)
+            for (uint32_t v = 0; v < (1u << wd[fld]); v++) {
+                const uint64_t m = (uint64_t)v << sh[fld];
+                uint32_t c = 0;
+                for (int by = 7; by >= 0; by--) c = ((c << 8) ^ crc16x8[((c >> 8) ^ (uint32_t)(m >> (8 * by))) & 0xffu]) & 0xffffu;
+                t11[at++] = (uint16_t)c;
+            }
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_t11), t11, sizeof t11);
+        if (e != hipSuccess) return e;
+    }
     return hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_xpow), xpow, 40 * sizeof(uint16_t));
 }
 
