@@ -2868,7 +2868,7 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
 #define TU_FN3(name, n) name##_tu##n
 #if BNF_TU == 1 || BNF_TU == 2 || BNF_TU == 5
 #define DEC_W (BNF_TU == 1 ? 8 : (BNF_TU == 5 ? 16 : 32))
-#define DEC_RD (BNF_TU == 2 ? 16 : 8) /* ring slots: LPC-32 subframes carry more bits per sample */
+#define DEC_RD 8 /* ring slots (16 for k_decode<32> measured: LDS then caps it at 6 waves per CU) */
 extern "C" {
 hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     return upload_tables(crc8, crc16x8, xpow);
