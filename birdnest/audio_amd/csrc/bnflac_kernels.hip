@@ -3121,12 +3121,12 @@ struct SideQ {
 };
 static std::mutex g_side_mu;
 static SideQ g_side[64];
-static int decode_fork_mode() { /* 0 serial; 1 fork after k_decode_st (default); 2 fork before it */
+static int decode_fork_mode() { /* 0 serial; 1 fork after k_decode_st; 2 fork before it (default) */
     static const int m = [] {
         const char *e = getenv("BNFLAC_DECODE_SERIAL");
         if (e && atoi(e) != 0) return 0;
         const char *f = getenv("BNFLAC_DECODE_FORK");
-        return (f && atoi(f) == 2) ? 2 : 1;
+        return (f && atoi(f) == 1) ? 1 : 2;
     }();
     return m;
 }
@@ -3193,13 +3193,12 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
     const uint32_t mode = ev_crc ? BNF_MODE_DEFER_CRC : 0u; /* a concurrent CRC pass is running (k_crc) */
     /* k_decode_st -> k_decode<8> on s (k_decode<8> takes k_decode_st's hand-backs);
      * k_decode<16> and k_decode<32> each on a side stream of the device, forked from s
-     * after k_decode_st and joined before anything that reads the whole batch: the classes
-     * are disjoint frame sets, and after k_decode_st (which fills the chip on its own) the
-     * three instances rarely do (C4: 15.7 + 9.8 + 7.9 ms serialised; 45 -> 41 ms).  Forking
-     * before k_decode_st (BNFLAC_DECODE_FORK=2) overlaps all four (C4 32 ms) but slows a
-     * batch with no W16/W32 frames (C2's k_decode_st +4%): the side launches' workgroups,
-     * early-exiting, still share the dispatcher and LDS slots with it; a high-priority
-     * stream for k_decode_st did not help.  The fork/join is enqueued under
+     * before k_decode_st (default) or after it (BNFLAC_DECODE_FORK=1), and joined before
+     * anything that reads the whole batch: the classes are disjoint frame sets.  Forking
+     * before overlaps all four (C4 35.7 -> 27.8 ms).  While k_decode<32> had a 16-slot ring
+     * (25.6 KB of LDS) its early-exiting workgroups slowed a batch with no W16/W32 frames
+     * (C2's k_decode_st +4%), so the fork came after k_decode_st; with the 8-slot ring
+     * (17 KB) C2 measures the same either way (3 A/B rounds).  The fork/join is enqueued under
      * one lock, so concurrent callers sharing the side streams keep their event pairs in
      * order. */
     /* Above 16 bits there are no stereo fast-path frames and LPC frames are W16/W32, so one

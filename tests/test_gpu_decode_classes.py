@@ -1,7 +1,7 @@
 """Decode-class split across streams (SURVEY.md 8a A10 dispatch; bnf_launch_decode).
 
 k_decode_st -> k_decode<8> run on the caller's stream, and k_decode<16> / k_decode<32> each
-on a side stream forked after k_decode_st (or before it, BNFLAC_DECODE_FORK=2).  k_decode<8>
+on a side stream forked before k_decode_st (or after it, BNFLAC_DECODE_FORK=1).  k_decode<8>
 takes k_decode_st's hand-backs (BNF_FL_REDO) also in blocks that belong to the other
 instances, which never look at stereo fast-path frames.
 These tests put hand-back-prone stereo frames, LPC-12 (W16) and LPC-32 (W32) frames into
@@ -89,7 +89,7 @@ sys.stdout.buffer.write(out.tobytes())
 
 
 @pytest.mark.skipif(not gpu_available(), reason="no GPU")
-@pytest.mark.parametrize("env", [{"BNFLAC_DECODE_SERIAL": "1"}, {"BNFLAC_DECODE_FORK": "2"}])
+@pytest.mark.parametrize("env", [{"BNFLAC_DECODE_SERIAL": "1"}, {"BNFLAC_DECODE_FORK": "1"}])
 def test_side_stream_matches_other_orders(env):
     data, offs, osmp, pcm, total = _mixed_batch(20)
     out, _ = _decode(data, offs, osmp, total)
