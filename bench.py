@@ -90,6 +90,9 @@ def parse_args():
     ap.add_argument("--no-index", action="store_true", help="skip the frame-indexer (bnflac_index_stream) timing")
     ap.add_argument("--no-reader", action="store_true", help="skip the streaming-reader (bnflac_reader_*) timing")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
+    ap.add_argument("--nccl-timeout", type=int, default=180, help="seconds before a stuck collective aborts the run")
+    ap.add_argument("--no-c5-flow", action="store_true",
+                    help="N > 1: skip the C5 shard -> index -> decode -> RCCL gather leg")
     ap.add_argument("--stats", action="store_true", help="report k_decode event counters (one extra step)")
     ap.add_argument("--ablate", default=None,
                     help="comma list of ablation bitmasks to time after the measurement (timing only, wrong output): "
@@ -541,6 +544,20 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
             "alg_bytes_rank": alg, "frames_rank": nframes}
 
 
+def c5_summary(r, args, world):
+    """value / timing / roofline fields of a c5_job result (the --config C5 line, or the C5 flow
+    leg of a multi-GPU C2 run)."""
+    step_ms = r["t_dec"] / args.steps * 1e3
+    out = {"value": round(r["samples"] * args.steps / r["t_dec"] / 1e6, 2), "unit": "MSamples/s",
+           "ms_per_step": round(step_ms, 4), "bitexact": r["ok"], "files": r["files"], "ranks": world,
+           "roofline": roofline(r["alg_bytes_rank"], r["t_launch"], 0.0, step_ms),
+           "with_gather": {"value": round(r["samples"] * args.steps / r["t_all"] / 1e6, 2), "unit": "MSamples/s",
+                           "ms_per_step": round(r["t_all"] / args.steps * 1e3, 4),
+                           "note": "each step: decode, then shard.gather_bytes of every rank's PCM to rank 0"}}
+    out["roofline"]["kernel"] = "k_parse + decode launch over the rank's files"
+    return out
+
+
 # --------------------------------------------------------------------------- main
 def main():
     args = parse_args()
@@ -551,9 +568,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # a stuck collective (barrier, timing reduction, the C5 gather) must end the run with a
+        # non-zero exit instead of hanging it: the watchdog aborts after the timeout
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
+                                timeout=datetime.timedelta(seconds=args.nccl_timeout))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
@@ -565,22 +587,15 @@ def main():
 
     if cfg == "C5":
         r = c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank)
-        step_ms = r["t_dec"] / args.steps * 1e3
-        line = {
-            "metric": METRIC, "value": round(r["samples"] * args.steps / r["t_dec"] / 1e6, 2), "unit": "MSamples/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_ms, 4),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
-            "data": "synthetic: deterministic generator (seeds 5 + 1000 i), BASELINE C5 file shape",
-            "config": {"workload": c["desc"] + f"; {r['files']} files sharded over {world} rank(s), "
-                                                "decode-only timing (gather reported beside it)",
-                       "files": r["files"], "parallelism": f"files sharded per rank x{world} + RCCL gather to rank 0"},
-            "bitexact": r["ok"],
-            "roofline": roofline(r["alg_bytes_rank"], r["t_launch"], 0.0, step_ms),
-            "with_gather": {"value": round(r["samples"] * args.steps / r["t_all"] / 1e6, 2), "unit": "MSamples/s",
-                            "ms_per_step": round(r["t_all"] / args.steps * 1e3, 4),
-                            "note": "each step: decode, then shard.gather_bytes of every rank's PCM to rank 0"},
-        }
-        line["roofline"]["kernel"] = "k_parse + decode launch over the rank's files"
+        line = {"metric": METRIC}
+        line.update(c5_summary(r, args, world))
+        line.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+                     "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+                     "data": "synthetic: deterministic generator (seeds 5 + 1000 i), BASELINE C5 file shape",
+                     "config": {"workload": c["desc"] + f"; {r['files']} files sharded over {world} rank(s), "
+                                                         "decode-only timing (gather reported beside it)",
+                                "files": r["files"],
+                                "parallelism": f"files sharded per rank x{world} + RCCL gather to rank 0"}})
         if rank == 0:
             js = json.dumps(line)
             print(js, flush=True)
@@ -661,6 +676,15 @@ def main():
         del wl
         torch.cuda.empty_cache()
         line["legs"] = {x: leg(x, args, torch, dev, libflac, synth, dec, stream) for x in legs}
+    elif world > 1 and not args.no_c5_flow:
+        # BASELINE config 5 at N GPUs: the files sharded over the ranks, each rank indexing and
+        # decoding its own, then the gather of every rank's PCM to rank 0 over RCCL
+        del wl
+        torch.cuda.empty_cache()
+        r = c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank)
+        line["legs"] = {"C5_flow": c5_summary(r, args, world)}
+        line["legs"]["C5_flow"]["config"] = {"workload": CONFIGS["C5"]["desc"], "files": r["files"],
+                                             "parallelism": f"files sharded per rank x{world} + RCCL gather to rank 0"}
     if rank == 0:
         js = json.dumps(line)
         print(js, flush=True)

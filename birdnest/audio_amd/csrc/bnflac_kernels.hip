@@ -167,9 +167,25 @@ DEV uint32_t ring_off(const BR &b, uint32_t w) { /* dword offset of word w from 
     return ((w & (b.wmask & ~3u)) << 6) + (w & 3u);
 }
 DEV uint32_t ring_word(const BR &b, uint32_t w) { return b.lring[ring_off(b, w)]; }
+/* LDS-DMA destination invariant.  A global_load_lds_dwordx4 writes lane l's 16 bytes at
+ * (destination base + 16 l); round 2 found that a base that is not 1 KiB aligned writes the
+ * wrong LDS bytes with no fault (wrong PCM).  Every ring slot row is one
+ * whole 1 KiB image, so the invariant is: ring bases 1 KiB aligned (LDS_DMA_ALIGN on every
+ * __shared__ ring) and slot offsets multiples of 1 KiB (the static_asserts below).  Debug
+ * builds (-DBNFLAC_DEBUG_ASSERTS) also check every base at run time. */
+#define LDS_DMA_ALIGN __attribute__((aligned(1024)))
+static_assert(RING_LANE_DW * 4 == 1024, "a ring slot row must be exactly one 1 KiB LDS-DMA image");
+DEV void dma_check_base(const lds_u32 *base) {
+#ifdef BNFLAC_DEBUG_ASSERTS
+    if (((uint32_t)(uintptr_t)base & 1023u) != 0u) __builtin_trap();
+#else
+    (void)base;
+#endif
+}
 DEV void dma_block(const BR &b, uint32_t j, uint32_t slot) { /* one 16-byte block per lane */
-    __builtin_amdgcn_global_load_lds((gvoid *)(b.w + (uint64_t)min(j, b.nblk - 1u) * 4u),
-                                     (lds_void *)(b.ring + slot * RING_LANE_DW), 16, 0, 0);
+    lds_u32 *dst = b.ring + slot * RING_LANE_DW;
+    dma_check_base(dst);
+    __builtin_amdgcn_global_load_lds((gvoid *)(b.w + (uint64_t)min(j, b.nblk - 1u) * 4u), (lds_void *)dst, 16, 0, 0);
 }
 
 /* Issue the blocks this lane will need next (exec-masked LDS-DMA per ring slot).  Blocks
@@ -1240,7 +1256,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
                                               uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate,
                                               uint32_t nparse, uint32_t ncrc, const uint32_t *__restrict__ perm,
                                               uint32_t keep_cn) {
-    __shared__ uint32_t ring[PARSE_RD * RING_LANE_DW]; /* parse: the bit ring; CRC: the tables */
+    __shared__ LDS_DMA_ALIGN uint32_t ring[PARSE_RD * RING_LANE_DW]; /* parse: the bit ring; CRC: the tables */
     static_assert(PARSE_RD * RING_LANE_DW * 4 >= (8 * 256 + 512) * 2, "CRC tables fit the ring");
     const uint32_t lane = threadIdx.x;
     const uint32_t tot = nparse + ncrc, b = blockIdx.x;
@@ -1520,7 +1536,7 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
                                                       bnf_frame_info *__restrict__ info,
                                                       const uint32_t *__restrict__ perm, uint32_t ablate) {
     static_assert(MAXW <= CHK && CHK % 8 == 0 && RD <= RING_MAX, "chunk must hold the predictor ring");
-    __shared__ uint32_t ring[RD * RING_LANE_DW];
+    __shared__ LDS_DMA_ALIGN uint32_t ring[RD * RING_LANE_DW];
     __shared__ int32_t lds[CHK * RP]; /* [sample][lane] */
     static_assert(CHK * RP >= 1024 + 512, "row buffer also holds the CRC tables and the tail's frame table");
     /* per-frame tables overlay the buffers while those are idle: the setup exchange uses
@@ -2625,7 +2641,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t ST_SPG = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u; /* stores per 4 samples */
     /* 16 KB: both channels' bitstream rings; in the tail, the 20 KB CRC-16 field tables */
-    __shared__ uint32_t ring[(2 * ST_RD * RING_LANE_DW > CRC11_N / 2) ? 2 * ST_RD * RING_LANE_DW : CRC11_N / 2];
+    __shared__ LDS_DMA_ALIGN uint32_t ring[(2 * ST_RD * RING_LANE_DW > CRC11_N / 2) ? 2 * ST_RD * RING_LANE_DW : CRC11_N / 2];
+    static_assert((ST_RD * RING_LANE_DW * 4) % 1024 == 0, "channel 1's ring base must stay 1 KiB aligned (LDS-DMA)");
 #ifdef BNF_ST_PAD
     __shared__ uint32_t occ_pad[BNF_ST_PAD]; /* experiment: LDS padding to cap waves per CU */
     if (ablate == 0xDEADu) occ_pad[threadIdx.x] = 1u;

@@ -267,11 +267,50 @@ template <typename T> bool hgrow(T *&p, size_t &cap, size_t n) { /* pinned host 
     return true;
 }
 
+/* Pool policy.  Only what open/close churn costs is worth keeping: the stream, events, ctx,
+ * index scratch and small buffers.  Buffers sized by the stream (the compressed copy, the PCM,
+ * the pinned ring slots and records) are kept only up to BNFLAC_READER_POOL_CAP bytes each
+ * (default 64 MiB), so a closed reader never pins a large stream's HBM or host memory for the
+ * life of the process; BNFLAC_READER_POOL=0 disables pooling; bnflac_reader_pool_release()
+ * frees everything pooled. */
+size_t pool_cap() {
+    static const size_t c = [] {
+        const char *e = getenv("BNFLAC_READER_POOL_CAP");
+        return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)64 << 20;
+    }();
+    return c;
+}
+bool pool_on() {
+    static const bool on = [] {
+        const char *e = getenv("BNFLAC_READER_POOL");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+void trim_for_pool(bnflac_reader *p) {
+    const size_t cap = pool_cap();
+    auto dtrim = [&](void *&b, size_t &c) {
+        if (b && c > cap) { (void)hipFree(b); b = nullptr; c = 0; }
+    };
+    dtrim(p->d_bytes, p->cap_bytes);
+    dtrim(p->d_out, p->cap_out);
+    dtrim(p->d_offs, p->cap_offs);
+    dtrim(p->d_os, p->cap_os);
+    dtrim(p->d_info, p->cap_info);
+    if (p->cap_ring > cap) {
+        for (int i = 0; i < 2; i++)
+            if (p->ring[i]) { (void)hipHostFree(p->ring[i]); p->ring[i] = nullptr; }
+        p->cap_ring = 0;
+    }
+    if (p->h_info && p->cap_hinfo > cap) { (void)hipHostFree(p->h_info); p->h_info = nullptr; p->cap_hinfo = 0; }
+}
+
 /* close: the resources go back to the pool (one set per device) unless the reader failed
  * in a way that may have left the stream in error */
 void release(bnflac_reader *r, bool keep = true) {
     bool ok = !r->stream || hipStreamSynchronize(r->stream) == hipSuccess;
-    if (keep && ok && r->ctx && r->stream && r->done[0] && r->done[1]) {
+    if (keep && ok && pool_on() && r->ctx && r->stream && r->done[0] && r->done[1]) {
+        trim_for_pool(r);
         std::lock_guard<std::mutex> lk(g_pool_mu);
         bool have = false;
         for (bnflac_reader *p : g_pool) have = have || p->device == r->device;
@@ -372,26 +411,6 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
         return rfail("bnflac_reader_open: the frame chain covers " + std::to_string(end) + " of " +
                      std::to_string(r->sp.total_samples) + " samples (damaged stream: use the libFLAC stream API)");
     }
-    if (!r->sp.total_samples && nf) {
-        /* length unknown (STREAMINFO total 0): a damaged frame would end the chain early with
-         * every chained frame intact.  Refuse when an acceptable header numbered past the
-         * chain's last frame follows it (trailing tags and metadata are allowed). */
-        const uint64_t last_no = last.number_type ? r->os[nf - 1] : last.number;
-        for (uint64_t p = last_off + 2; p + 1 < nbytes; p++) {
-            uint64_t no = 0;
-            uint32_t is_sample = 0;
-            if (bytes[p] != 0xFF || !header_ok(bytes, nbytes, p, &no, &is_sample)) continue;
-            const uint64_t room = (nbytes - p) / 16 + 1; /* frames that could still follow */
-            const bool plausible = is_sample ? (no >= end && no <= end + room * 65536ull)
-                                             : (no > last_no && no <= last_no + 1 + room);
-            if (plausible) {
-                release(r);
-                return rfail("bnflac_reader_open: the frame chain ends at byte " + std::to_string(last_off) +
-                             " but a frame header follows at byte " + std::to_string(p) +
-                             " (damaged stream: use the libFLAC stream API)");
-            }
-        }
-    }
     tr.mark("index-readback", r->stream);
     r->total_bytes = end * r->stride;
     r->nwin = (nf + r->window - 1) / r->window;
@@ -416,6 +435,35 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
         const std::string e = bnflac_last_error();
         release(r, false);
         return rfail("bnflac_reader_open: " + e);
+    }
+    if (!r->sp.total_samples && nf) {
+        /* length unknown (STREAMINFO total 0): a damaged frame would end the chain early with
+         * every chained frame intact.  Refuse when an acceptable header numbered past the
+         * chain's last frame follows it (trailing tags and metadata are allowed).  The scan
+         * starts where the last frame ends (its decoded record's resume bit: after the CRC-16
+         * footer), so a header-like byte pattern inside that frame's own payload is never taken
+         * for a following frame; this needs the decode, so these streams sync once here. */
+        if (hipStreamSynchronize(r->stream) != hipSuccess) {
+            release(r, false);
+            return rfail("bnflac_reader_open: HIP error while decoding");
+        }
+        const bnflac_frame_info &lf = r->h_info[nf - 1];
+        const uint64_t scan0 = (lf.status == 0 && lf.resume_bit / 8 > last_off) ? lf.resume_bit / 8 : last_off + 2;
+        const uint64_t last_no = last.number_type ? r->os[nf - 1] : last.number;
+        for (uint64_t p = scan0; p + 1 < nbytes; p++) {
+            uint64_t no = 0;
+            uint32_t is_sample = 0;
+            if (bytes[p] != 0xFF || !header_ok(bytes, nbytes, p, &no, &is_sample)) continue;
+            const uint64_t room = (nbytes - p) / 16 + 1; /* frames that could still follow */
+            const bool plausible = is_sample ? (no >= end && no <= end + room * 65536ull)
+                                             : (no > last_no && no <= last_no + 1 + room);
+            if (plausible) {
+                release(r);
+                return rfail("bnflac_reader_open: the frame chain ends at byte " + std::to_string(last_off) +
+                             " but a frame header follows at byte " + std::to_string(p) +
+                             " (damaged stream: use the libFLAC stream API)");
+            }
+        }
     }
     if (issue_window(r, 0) || issue_window(r, 1)) {
         release(r, false);
@@ -579,13 +627,18 @@ BNFLAC_API int64_t bnflac_reader_read_filereader(bnflac_reader *r, uint8_t *buff
     }
     while ((uint64_t)copied < num_bytes) {
         if (r->eos) break;
-        if (r->sp.bps != 16 && r->sp.bps != 24) { /* the first frame decodes, its copy throws */
+        if (r->sp.bps != 16 && r->sp.bps != 24) {
+            /* ProcessSingle decodes the frame; CopyFlacBufferToNAudioBuffer throws from its
+             * sample loop (FLACFileReader.cs:239-240), which runs only while the offset is
+             * inside the buffer (:211-214): at or past buffer.Length it copies 0 bytes and
+             * Read keeps decoding to the end of the stream */
             if (r->fr_next >= r->nframes) {
                 r->eos = true;
                 break;
             }
             r->fr_next++;
-            return rfail("Input FLAC bit depth is not supported!");
+            if (noff < buffer_length) return rfail("Input FLAC bit depth is not supported!");
+            continue;
         }
         const uint8_t *fb = nullptr;
         uint32_t bs = 0;
@@ -610,6 +663,27 @@ BNFLAC_API void bnflac_reader_close(bnflac_reader *r) {
     if (!r) return;
     RDevGuard dg(r->device);
     release(r, !r->failed);
+}
+
+BNFLAC_API int bnflac_reader_pool_release(int device) {
+    std::vector<bnflac_reader *> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size();) {
+            if (device < 0 || g_pool[i]->device == device) {
+                drop.push_back(g_pool[i]);
+                g_pool.erase(g_pool.begin() + (long)i);
+            } else {
+                i++;
+            }
+        }
+    }
+    for (bnflac_reader *p : drop) {
+        RDevGuard dg(p->device);
+        free_resources(p);
+        delete p;
+    }
+    return (int)drop.size();
 }
 
 } /* extern "C" */

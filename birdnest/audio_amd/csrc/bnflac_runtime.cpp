@@ -309,7 +309,16 @@ extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d
         return fail("bnflac_decode_parsed: out of device memory (decode-order scratch)");
     /* the records of this call came from bnflac_parse_frames with the concurrent CRC pass:
      * the decode defers the check to k_crc_join after it */
-    hipEvent_t ev = (ctx->pending_info == d_info && ctx->pending_n == nframes) ? ctx->ev_crc : nullptr;
+    const bool match = ctx->pending_info == d_info && ctx->pending_n == nframes;
+    hipEvent_t ev = match ? ctx->ev_crc : nullptr;
+    if (!match && ctx->pending_info) {
+        /* another record array (or a subset of the pending one) while k_crc may still be
+         * writing crc_next: the decode must not read a crc_next k_crc has not written yet
+         * (it would trust a stale VALID|ZERO word and skip the CRC-16 check), so it waits for
+         * the pass to finish and checks the frames itself */
+        if (hipStreamWaitEvent((hipStream_t)hs, ctx->ev_crc, 0) != hipSuccess)
+            return fail("bnflac_decode_parsed: cannot wait for the CRC pass");
+    }
     ctx->pending_info = nullptr;
     hipError_t e = bnf_launch_decode((const uint32_t *)d_bytes, nbytes, nframes, p,
                                      lanes_for(sp->channels), out_format, d_out, out_bytes, (bnf_frame_info *)d_info,

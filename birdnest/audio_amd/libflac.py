@@ -127,7 +127,8 @@ BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error",
                  "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats", "bnflac_debug_set_crc_pass",
                  "bnflac_md5_interleaved32", "bnflac_index_stream"]
 READER_SYMBOLS = ["bnflac_reader_open", "bnflac_reader_params", "bnflac_reader_read", "bnflac_reader_close",
-                  "bnflac_reader_last_error", "bnflac_reader_seek", "bnflac_reader_read_filereader"]
+                  "bnflac_reader_last_error", "bnflac_reader_seek", "bnflac_reader_read_filereader",
+                  "bnflac_reader_pool_release"]
 
 _LIB = None
 
@@ -191,6 +192,8 @@ def load() -> ctypes.CDLL:
     L.bnflac_reader_read.restype = ctypes.c_int64
     L.bnflac_reader_read.argtypes = [p, p, ctypes.c_uint64]
     L.bnflac_reader_close.argtypes = [p]
+    L.bnflac_reader_pool_release.argtypes = [ctypes.c_int]
+    L.bnflac_reader_pool_release.restype = ctypes.c_int
     L.bnflac_reader_read_filereader.restype = ctypes.c_int64
     L.bnflac_reader_read_filereader.argtypes = [p, p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
     L.bnflac_reader_seek.restype = i

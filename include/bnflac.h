@@ -232,6 +232,12 @@ BNFLAC_API int bnflac_reader_seek(bnflac_reader *reader, uint64_t sample);
 BNFLAC_API int64_t bnflac_reader_read_filereader(bnflac_reader *reader, uint8_t *buffer, uint64_t offset,
                                                  uint64_t num_bytes, uint64_t buffer_length);
 BNFLAC_API void bnflac_reader_close(bnflac_reader *reader);
+/* A closed reader's stream, events and small buffers stay pooled per device for the next
+ * open (buffers above BNFLAC_READER_POOL_CAP bytes, default 64 MiB, are freed on close;
+ * BNFLAC_READER_POOL=0 turns pooling off).  This frees every pooled resource of `device`
+ * (-1: of every device), e.g. before handing the GPU's memory to another user.  Returns the
+ * number of pooled reader sets freed. */
+BNFLAC_API int bnflac_reader_pool_release(int device);
 BNFLAC_API const char *bnflac_reader_last_error(void);
 
 #ifdef __cplusplus

@@ -647,6 +647,44 @@ def test_filereader_mode_quirks_24bit(gpu):
         _filereader_vs_oracle(libflac, s.data.tobytes(), windows=(2, 64))
 
 
+@pytest.mark.parametrize("name", ["mono_8bit_fixed", "odd_headers_20bit"])
+def test_filereader_mode_unsupported_depth_offset_at_end(gpu, tmp_path, name):
+    """NotSupported is thrown from CopyFlacBufferToNAudioBuffer's sample loop
+    (FLACFileReader.cs:214-240), which never runs with the offset at buffer.Length: Read then
+    returns 0 per frame and ProcessSingle runs to the end of the stream.  The native compat
+    mode must agree with the C# mirror over the libFLAC-compatible API (and throw as soon as
+    the offset is inside the buffer)."""
+    from birdnest.audio_amd import flac_file_reader
+    torch, libflac, _ = gpu
+    data = _read(name)
+    path = os.path.join(str(tmp_path), name + ".flac")
+    open(path, "wb").write(data)
+    buf = bytearray(4096)
+    mirror = flac_file_reader.FLACFileReader(path)
+    try:
+        want = [mirror.Read(buf, len(buf), 64), mirror.Read(buf, len(buf), 64)]
+    finally:
+        mirror.Dispose()
+    mirror = flac_file_reader.FLACFileReader(path)
+    try:
+        with pytest.raises(flac_file_reader.NotSupportedException):
+            mirror.Read(buf, 0, 64)
+    finally:
+        mirror.Dispose()
+    r = libflac.Reader(data, libflac.OUT_FILEREADER, window_frames=3)
+    try:
+        got = [r.ReadFileReader(buf, len(buf), 64), r.ReadFileReader(buf, len(buf), 64)]
+    finally:
+        r.close()
+    assert got == want == [0, 0]
+    r = libflac.Reader(data, libflac.OUT_FILEREADER, window_frames=3)
+    try:
+        with pytest.raises(RuntimeError, match="bit depth is not supported"):
+            r.ReadFileReader(buf, 0, 64)
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("window,chunk", [(256, 16384), (7, 1000), (1, 4096 * 4 + 3)])
 def test_reader_c2_windows_and_chunks(gpu, window, chunk):
     from birdnest.audio_amd import synth
@@ -857,3 +895,13 @@ def test_reader_pool_reuse_across_sizes_and_layouts(gpu):
     finally:
         a.close()
         b.close()
+    # one pooled set per device; releasing it frees it, and the next open allocates afresh
+    L = libflac.load()
+    assert L.bnflac_reader_pool_release(-1) == 1
+    assert L.bnflac_reader_pool_release(-1) == 0
+    r = libflac.Reader(c2.data.tobytes(), libflac.OUT_FLACDECODER, window_frames=16)
+    try:
+        assert r.read_all(16384) == want_c2
+    finally:
+        r.close()
+    assert L.bnflac_reader_pool_release(0) == 1

@@ -144,6 +144,41 @@ def test_seektable_narrows_seek_and_matches_oracle(gpu, cfg, kw, every, seeks):
         assert st_tab["read_total"] < st_plain["read_total"], (st_tab, st_plain)
 
 
+def _vbr_stream(nframes=400):
+    """A variable-bitrate C2-shaped stream: the first half of the frames from a near-silent
+    encode, the second half from a loud, noisy one (same blocksize, so the spliced frames keep
+    consecutive frame numbers and their own CRCs).  Byte position is then far from linear in
+    the sample number, which is what a SEEKTABLE is for."""
+    import types
+    from birdnest.audio_amd import synth
+    a = synth.encode(synth.config("C2", nframes=nframes, last_blocksize=0, level=0.0001, noise=0.000002, seed=21))
+    b = synth.encode(synth.config("C2", nframes=nframes, last_blocksize=0, level=0.95, noise=0.3, seed=22))
+    h = nframes // 2
+    ca, cb = int(a.frame_offsets[h]), int(b.frame_offsets[h])
+    data = a.data.tobytes()[:ca] + b.data.tobytes()[cb:]
+    offs = np.concatenate([a.frame_offsets[:h], b.frame_offsets[h:] - cb + ca]).astype(np.uint64)
+    pcm = np.concatenate([a.pcm[:h * 4096], b.pcm[h * 4096:]])
+    return data, types.SimpleNamespace(params=a.params, frame_offsets=offs, pcm=pcm)
+
+
+def test_seektable_reduces_probes_on_variable_bitrate(gpu):
+    """On a stream whose bitrate changes about 8-fold half way, the table-free interpolation search
+    guesses badly; with a SEEKTABLE libFLAC's search starts from the bracketing points and takes
+    strictly fewer client seeks.  Output equals the oracle's (which ignores the table) and the
+    source PCM either way."""
+    plain, s = _vbr_stream()
+    assert int(s.frame_offsets[-1] - s.frame_offsets[200]) > 6 * int(s.frame_offsets[200] - s.frame_offsets[0])
+    data = _with_seektable(plain, s, 8)
+    seeks = [(-1, 150 * 4096 + 33), (2, 330 * 4096 + 7), (4, 260 * 4096)]
+    _compare(gpu, data, seeks)
+    st_tab, st_plain = {}, {}
+    ev_t, pcm_t = gpu.run(data, seeks=seeks, stats=st_tab)
+    ev_p, pcm_p = gpu.run(plain, seeks=seeks, stats=st_plain)
+    assert np.array_equal(pcm_t, pcm_p)
+    assert st_tab["seek_calls"] < st_plain["seek_calls"], (st_tab, st_plain)
+    assert st_tab["read_total"] < st_plain["read_total"], (st_tab, st_plain)
+
+
 @pytest.mark.parametrize("shift", [-5000, 3, 1 << 40])
 def test_misleading_seektable_same_output(gpu, shift):
     """A table whose offsets are wrong (before, inside or past the stream) costs a
