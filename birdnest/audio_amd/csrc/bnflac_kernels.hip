@@ -386,21 +386,131 @@ DEV uint8_t crc8_bytes(const uint8_t *p, uint32_t n) {
     return c;
 }
 
+/* ------------------------------------------------------ wave-uniform bit reader */
+/* The reader of the wave-per-frame kernels (k_parse_wave): one cursor for the whole wave
+ * (every lane holds the same value), over a ring of WR_SLOTS windows of 256 stream words in
+ * LDS.  Window j holds words [w0 + 256 j, w0 + 256 j + 256) and sits in slot j % WR_SLOTS; one
+ * global_load_lds_dwordx4 fills it (64 lanes x 16 B, coalesced).  Windows are fetched ahead
+ * of the cursor (up to WR_SLOTS - 1) and waited for with an exact vmcnt: the wave issues no
+ * other vector-memory ops while it reads.  Header fields are read at the uniform cursor
+ * (two broadcast LDS reads per field); the Rice scan (wave_rice_skip) reads each lane's own
+ * segment words from the same ring. */
+#define WR_SLOTS 8 /* a 16-word-per-lane scan pass spans 5 windows */
+#define WR_WIN 256u /* words per window (1 KiB) */
+struct WR {
+    const uint32_t *__restrict__ w;
+    uint32_t nblk;   /* 16-byte blocks readable */
+    lds_u32 *ring;   /* WR_SLOTS KiB, 1 KiB aligned */
+    uint32_t w0;     /* stream word of window 0 (multiple of WR_WIN) */
+    uint32_t issued; /* windows issued (0 .. issued-1) */
+    uint32_t landed; /* windows known to have landed */
+    uint64_t pos;    /* bit cursor (absolute, MSB-first) */
+    uint64_t st[8];  /* debug counters (g_pw_stats layout), flushed once per wave */
+};
+DEV uint32_t wr_u(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+DEV void wr_issue(WR &r) { /* window r.issued into its slot */
+    const uint32_t j = r.issued++;
+    lds_u32 *dst = r.ring + (j % WR_SLOTS) * WR_WIN;
+    dma_check_base(dst);
+    const uint32_t blk = (r.w0 >> 2) + j * (WR_WIN / 4u) + (threadIdx.x & 63u);
+    __builtin_amdgcn_global_load_lds((gvoid *)(r.w + (uint64_t)min(blk, r.nblk - 1u) * 4u), (lds_void *)dst, 16, 0, 0);
+}
+DEV void wr_reset(WR &r, uint32_t wa) {
+    wait_vm();
+    r.w0 = wa & ~(WR_WIN - 1u);
+    r.issued = r.landed = 0;
+}
+DEV void wr_init(WR &r, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, uint64_t bit) {
+    r.w = words;
+    r.nblk = (uint32_t)((nbytes + 15u) >> 4);
+    r.ring = ring;
+    r.pos = bit;
+    r.w0 = wr_u((uint32_t)(bit >> 5)) & ~(WR_WIN - 1u);
+    r.issued = r.landed = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.st[i] = 0;
+}
+/* words [wa, wb] readable (wb - wa < WR_SLOTS - 2 windows); fetches ahead */
+DEV void wr_need(WR &r, uint32_t wa, uint32_t wb) {
+    wa = wr_u(wa);
+    wb = wr_u(wb);
+    if (wa < r.w0 || ((wa - r.w0) / WR_WIN) > r.issued + 2u) wr_reset(r, wa);
+    const uint32_t lo = (wa - r.w0) / WR_WIN, hi = (wb - r.w0) / WR_WIN;
+    while (r.issued < lo + WR_SLOTS) wr_issue(r);
+    if (hi >= r.landed) { /* at most WR_SLOTS - 1 younger windows may stay in flight */
+        switch (wr_u(r.issued - 1u - hi)) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        }
+        r.landed = hi + 1u;
+    }
+}
+static_assert(WR_SLOTS == 8, "wr_need's vmcnt switch covers WR_SLOTS - 1 windows in flight");
+DEV uint32_t wr_word(const WR &r, uint32_t w) { return __builtin_bswap32(r.ring[(w - r.w0) & (WR_SLOTS * WR_WIN - 1u)]); }
+DEV uint32_t wr_peek(WR &r) { /* the 32 bits at the cursor */
+    const uint32_t wi = (uint32_t)(r.pos >> 5);
+    wr_need(r, wi, wi + 1u);
+    const uint32_t hi = wr_u(wr_word(r, wi)), lo = wr_u(wr_word(r, wi + 1u));
+    const uint32_t s = (uint32_t)r.pos & 31u;
+    return s ? __builtin_amdgcn_alignbit(hi, lo, 32u - s) : hi;
+}
+DEV uint64_t br_pos(const WR &r) { return r.pos; }
+DEV uint32_t br_peek(WR &r) { return wr_peek(r); }
+DEV void br_seek(WR &r, uint64_t bit) { r.pos = bit; }
+DEV void br_skip(WR &r, uint64_t n) { r.pos += n; }
+DEV uint32_t br_read(WR &r, uint32_t n) { /* 0..32 bits */
+    const uint32_t v = n ? (wr_peek(r) >> ((32u - n) & 31u)) : 0u;
+    r.pos += n;
+    return v;
+}
+DEV int32_t br_read_s(WR &r, uint32_t n) {
+    const uint32_t v = br_read(r, n), s = (32u - n) & 31u;
+    return (int32_t)(v << s) >> s;
+}
+DEV bool br_unary(WR &r, uint32_t &q, uint64_t limit) { /* read_unary_unsigned @0x10001960 */
+    uint32_t acc = 0;
+    for (;;) {
+        const uint32_t p = wr_peek(r);
+        if (p) {
+            const uint32_t z = (uint32_t)__builtin_clz(p);
+            r.pos += z + 1u;
+            q = acc + z;
+            return true;
+        }
+        acc += 32u;
+        r.pos += 32u;
+        if (r.pos > limit) {
+            q = acc;
+            return false;
+        }
+    }
+}
+
 /* ------------------------------------------------------------ frame header */
 enum { E_LOST_SYNC = 0, E_BAD_HEADER = 1, E_CRC = 2, E_UNPARSEABLE = 3 };
 
 /* read_frame_header_ @0x10011d70: fills fi; returns BNF_ST_* (OK also when the header
  * is flagged unparseable -- the caller reports that after the number conversion). */
-DEV uint32_t parse_header(BR &b, uint64_t fbit, uint64_t limit, const bnf_stream_params &sp,
+template <class R> /* R: BR (lane cursor) or WR (wave-uniform cursor) */
+DEV uint32_t parse_header(R &b, uint64_t fbit, uint64_t limit, const bnf_stream_params &sp,
                           bnf_frame_info &fi) {
-    uint8_t raw[16];
-    uint32_t rawlen = 2;
+    /* the header's CRC-8 is folded in as each byte is read (no byte buffer: a per-lane array
+     * indexed at run time would live in scratch memory) */
+    uint32_t crc = 0, last = 0, b2 = 0, b3 = 0;
+    auto take = [&](uint32_t v) { crc = g_crc8_tab[crc ^ v]; last = v; };
     uint32_t unparseable = 0, bs_hint = 0, sr_hint = 0, x;
     br_seek(b, fbit);
-    raw[0] = (uint8_t)br_read(b, 8);
-    raw[1] = (uint8_t)br_read(b, 8);
+    take(br_read(b, 8));
+    const uint32_t b1 = br_read(b, 8);
+    take(b1);
     fi.cached = -1;
-    if (raw[1] & 0x02) unparseable = 1;
+    if (b1 & 0x02) unparseable = 1;
     for (int i = 0; i < 2; i++) {
         x = br_read(b, 8);
         if (x == 0xff) {
@@ -409,15 +519,17 @@ DEV uint32_t parse_header(BR &b, uint64_t fbit, uint64_t limit, const bnf_stream
             fi.resume_bit = br_pos(b);
             return BNF_ST_ERROR;
         }
-        raw[rawlen++] = (uint8_t)x;
+        take(x);
+        if (i == 0) b2 = x;
+        else b3 = x;
     }
-    x = raw[2] >> 4;
+    x = b2 >> 4;
     if (x == 0) unparseable = 1;
     else if (x == 1) fi.blocksize = 192;
     else if (x <= 5) fi.blocksize = 576u << (x - 2);
     else if (x <= 7) bs_hint = x;
     else fi.blocksize = 256u << (x - 8);
-    x = raw[2] & 0x0f;
+    x = b2 & 0x0f;
     switch (x) {
     case 0:
         if (sp.has_stream_info) fi.sample_rate = sp.sample_rate;
@@ -440,7 +552,7 @@ DEV uint32_t parse_header(BR &b, uint64_t fbit, uint64_t limit, const bnf_stream
         return BNF_ST_ERROR;
     default: sr_hint = x; break;
     }
-    x = (uint32_t)(raw[3] >> 4);
+    x = b3 >> 4;
     if (x & 8) {
         fi.channels = 2;
         if ((x & 7) <= 2) fi.assignment = (x & 7) + 1;
@@ -449,7 +561,7 @@ DEV uint32_t parse_header(BR &b, uint64_t fbit, uint64_t limit, const bnf_stream
         fi.channels = x + 1;
         fi.assignment = 0;
     }
-    x = (uint32_t)(raw[3] & 0x0e) >> 1;
+    x = (b3 & 0x0e) >> 1;
     switch (x) {
     case 0:
         if (sp.has_stream_info) fi.bps = sp.bps;
@@ -462,15 +574,15 @@ DEV uint32_t parse_header(BR &b, uint64_t fbit, uint64_t limit, const bnf_stream
     case 6: fi.bps = 24; break;
     default: unparseable = 1; break;
     }
-    if (raw[3] & 0x01) unparseable = 1;
+    if (b3 & 0x01) unparseable = 1;
     /* UTF-8 frame/sample number (@0x10001e20 / @0x10001f60), with libFLAC's truthiness tests */
-    const bool is64 = (raw[1] & 0x01) || (sp.has_stream_info && sp.min_blocksize != sp.max_blocksize);
+    const bool is64 = (b1 & 0x01) || (sp.has_stream_info && sp.min_blocksize != sp.max_blocksize);
     {
         uint64_t v = 0;
         uint32_t n;
         bool bad = false;
         x = br_read(b, 8);
-        raw[rawlen++] = (uint8_t)x;
+        take(x);
         if (!(x & 0x80)) { v = x; n = 0; }
         else if ((x & 0xC0) && !(x & 0x20)) { v = x & 0x1F; n = 1; }
         else if ((x & 0xE0) && !(x & 0x10)) { v = x & 0x0F; n = 2; }
@@ -481,13 +593,13 @@ DEV uint32_t parse_header(BR &b, uint64_t fbit, uint64_t limit, const bnf_stream
         else { bad = true; n = 0; }
         for (; !bad && n; n--) {
             x = br_read(b, 8);
-            raw[rawlen++] = (uint8_t)x;
+            take(x);
             if (!(x & 0x80) || (x & 0x40)) bad = true;
             else v = (v << 6) | (x & 0x3F);
         }
         if (!is64 && !bad) v &= 0xffffffffull; /* 32-bit accumulation (6 bytes max => 31 bits) */
         if (bad) {
-            fi.cached = raw[rawlen - 1];
+            fi.cached = (int32_t)last;
             fi.err = E_BAD_HEADER;
             fi.resume_bit = br_pos(b);
             return BNF_ST_ERROR;
@@ -497,20 +609,20 @@ DEV uint32_t parse_header(BR &b, uint64_t fbit, uint64_t limit, const bnf_stream
     }
     if (bs_hint) {
         x = br_read(b, 8);
-        raw[rawlen++] = (uint8_t)x;
+        take(x);
         if (bs_hint == 7) {
             uint32_t y = br_read(b, 8);
-            raw[rawlen++] = (uint8_t)y;
+            take(y);
             x = (x << 8) | y;
         }
         fi.blocksize = x + 1;
     }
     if (sr_hint) {
         x = br_read(b, 8);
-        raw[rawlen++] = (uint8_t)x;
+        take(x);
         if (sr_hint != 12) {
             uint32_t y = br_read(b, 8);
-            raw[rawlen++] = (uint8_t)y;
+            take(y);
             x = (x << 8) | y;
         }
         fi.sample_rate = (sr_hint == 12) ? x * 1000u : (sr_hint == 13 ? x : x * 10u);
@@ -518,7 +630,7 @@ DEV uint32_t parse_header(BR &b, uint64_t fbit, uint64_t limit, const bnf_stream
     x = br_read(b, 8);
     fi.crc8 = x;
     if (br_pos(b) > limit) return BNF_ST_TRUNC;
-    if (crc8_bytes(raw, rawlen) != (uint8_t)x) {
+    if (crc != (x & 0xffu)) {
         fi.err = E_BAD_HEADER;
         fi.resume_bit = br_pos(b);
         return BNF_ST_ERROR;
@@ -559,8 +671,8 @@ struct SubHdr {
  * STORE: warm-ups go to warm[u * WS] and coefficients to coef[u] for u < NW, in loops
  * unrolled to NW (compile-time indices: register arrays stay in registers).  Returns
  * BNF_ST_*; on ERROR sets err and the reader position is where libFLAC stops. */
-template <bool STORE, int NW = 32, int WS = 1>
-DEV uint32_t parse_subframe_head(BR &b, uint32_t bps, uint32_t bs, uint64_t limit, SubHdr &h,
+template <bool STORE, int NW = 32, int WS = 1, class R = BR>
+DEV uint32_t parse_subframe_head(R &b, uint32_t bps, uint32_t bs, uint64_t limit, SubHdr &h,
                                  int32_t *warm, int32_t *coef, int32_t &err) {
     uint32_t x = br_read(b, 8);
     uint32_t wflag = x & 1u;
@@ -716,6 +828,234 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
         skip_step(b, rem, k, k1, km, p, parts, tr, limit);
     }
     return (tr || br_pos(b) > limit) ? BNF_ST_TRUNC : BNF_ST_OK;
+}
+
+/* ------------------------------------------- wave-cooperative Rice boundary scan */
+/* Skip `cnt` Rice codewords of parameter k (k + 1 = k1) from the wave-uniform cursor r.pos,
+ * with the whole wave on one partition (option ii; north_star's
+ * "wavefront prefix-scan for the Rice bit-cursor").  One pass covers 64 stream words: lane i
+ * owns the 32 bits of word ws + i (ws = the cursor's word) and can see the next two words.
+ *  1. Speculation: every lane decodes codeword lengths from the start of its word (lane 0
+ *     from the true cursor), recording the codeword starts it visits in a 32-bit mask and the
+ *     first start at or past the word's end (`exit`, relative to the word: 32..94).
+ *  2. Splice: lane i's true entry is lane i-1's exit - 32.  A lane whose entry was not its
+ *     speculative one re-decodes from it until it lands on a start in its mask (Rice decoding
+ *     from a given position is deterministic, so from there the paths coincide) or leaves the
+ *     word (its exit changed: the next lane re-checks).  Repeated until no exit changes;
+ *     lane 0 is always right, so the loop ends within 64 rounds (in practice 1-3).
+ *  3. Count: an inclusive wave scan of the per-lane counts gives the codeword index at every
+ *     word; if the partition ends inside the pass, the lane holding its last codeword finds the
+ *     end (the next codeword start), otherwise the cursor moves to lane 63's exit.
+ * A window of 32 zero bits (a unary prefix >= 32, rare: escapes exist for such values) sends
+ * the rest of the partition to a uniform serial walk (wave_rice_skip_serial).  Returns false
+ * when that walk runs past `limit` (libFLAC's reader would block: TRUNC). */
+DEV bool wave_rice_skip_serial(WR &r, uint32_t cnt, uint32_t k, uint64_t limit) {
+    for (; cnt; cnt--) {
+        uint32_t q;
+        if (!br_unary(r, q, limit)) return false;
+        r.pos += k;
+    }
+    return true;
+}
+/* DPP lane moves (wave_shr:1 and the row_shr / row_bcast steps of an inclusive wave scan):
+ * VALU-latency exchanges instead of ds_bpermute round trips through the LDS queue */
+DEV uint32_t dpp_prev(uint32_t x) { /* lane i gets lane i-1's x; lane 0 gets 0 */
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, true);
+}
+DEV uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true); /* row_shr:1 */
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true); /* row_shr:2 */
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true); /* row_shr:4 */
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true); /* row_shr:8 */
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); /* row_bcast:15 */
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); /* row_bcast:31 */
+    return x;
+}
+/* debug counters of the wave scan (k_parse_wave's `stats` argument; BNFLAC_PW_STATS=1):
+ * 0 passes, 1 splice rounds, 2 serial fallbacks, 3 partitions, 4 frames, 5 wave-cycles (s_memtime) in scans,
+ * 6 of them in window waits, 7 in splices */
+__device__ unsigned long long g_pw_stats[8];
+DEV void pw_stat(WR &r, bool on, int i, unsigned long long v = 1ull) {
+    if (on) r.st[i] += v;
+}
+DEV void pw_flush(const WR &r, bool on) {
+    if (on && (threadIdx.x & 63u) == 0u) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) atomicAdd(&g_pw_stats[i], (unsigned long long)r.st[i]);
+    }
+}
+/* One lane's segment walk: SW stream words (w[0..SW-1]; w[SW] holds the following word, for
+ * prefixes that cross the segment's end).  From bit `pos` (relative to w[0]'s first bit) it
+ * measures codeword lengths (q + 1 + k; the k low bits are not read) and sets the start bit of
+ * every codeword that starts inside the segment in nm[].  STOP: stop at a start already in om[]
+ * (the rest of that path is known).  Unrolled per word so every register index is static.
+ * Returns the first start at or past the segment's end (32 SW .. 32 SW + 62), or the stop point. */
+template <int SW, bool STOP>
+DEV uint32_t seg_walk(const uint32_t (&w)[SW + 1], uint32_t pos, uint32_t k1, uint32_t nsteps, const uint32_t (&om)[SW],
+                      uint32_t (&nm)[SW], bool &slow, bool &merged) {
+    /* Straight-line, predicated steps (no divergent loop): at most nsteps = floor(31 / k1) + 1
+     * codewords start in one word (wave-uniform), so word j runs nsteps steps and a lane whose
+     * cursor has left the word (or stopped) advances 0.  A word is skipped when no lane is
+     * still inside it. */
+#pragma unroll
+    for (int j = 0; j < SW; j++) nm[j] = 0u;
+    slow = merged = false;
+#pragma unroll
+    for (int j = 0; j < SW; j++) {
+        const uint32_t lo = 32u * (uint32_t)j, hi = lo + 32u;
+        if (!any_lane(!merged && !slow && pos < hi)) continue;
+        const uint64_t pair = ((uint64_t)w[j] << 32) | w[j + 1];
+        for (uint32_t t = 0; t < nsteps; t++) { /* uniform trip count */
+            const uint32_t rb = pos - lo; /* in [0, 32) while the cursor is in this word */
+            const bool in = !merged && !slow && pos < hi;
+            const bool stop = STOP && in && ((om[j] >> (rb & 31u)) & 1u);
+            const uint32_t q = ffbh((uint32_t)((pair << (rb & 31u)) >> 32));
+            const bool sl = q >= 32u;
+            const bool act = in && !stop && !sl;
+            nm[j] |= act ? (1u << (rb & 31u)) : 0u;
+            pos += act ? q + k1 : 0u;
+            merged = merged || stop;
+            slow = slow || (in && !stop && sl);
+        }
+    }
+    return pos;
+}
+template <int SW>
+DEV bool wave_rice_skip(WR &r, uint32_t cnt, uint32_t k, uint64_t limit, bool stats = false) {
+    constexpr uint32_t SB = 32u * SW; /* bits per lane per pass */
+    const uint32_t lane = threadIdx.x & 63u, k1 = k + 1u;
+    pw_stat(r, stats, 3);
+    while (cnt) {
+        pw_stat(r, stats, 0);
+        const uint64_t p = r.pos;
+        if (p > limit) return true; /* the caller reports TRUNC from the position */
+        const uint32_t ws = wr_u((uint32_t)(p >> 5)), e0 = (uint32_t)p & 31u;
+        const uint64_t tw0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+        wr_need(r, ws, ws + 64u * SW);
+        if (stats) pw_stat(r, true, 6, __builtin_amdgcn_s_memtime() - tw0);
+        uint32_t w[SW + 1];
+#pragma unroll
+        for (int j = 0; j <= SW; j++) w[j] = wr_word(r, ws + SW * lane + (uint32_t)j);
+        /* 1. speculative walk of this lane's segment from its first bit (lane 0: the cursor).
+         * `slow` only matters if the lane turns out to lie inside the partition. */
+        uint32_t ent = lane ? 0u : e0;
+        uint32_t m[SW], none[SW];
+#pragma unroll
+        for (int j = 0; j < SW; j++) none[j] = 0u;
+        bool slow, merged;
+        const uint32_t nsteps = 31u / k1 + 1u; /* codeword starts per word, at most */
+        uint32_t exit = seg_walk<SW, false>(w, ent, k1, nsteps, none, m, slow, merged);
+        if (slow) exit = SB;
+        /* 2. splice: a lane whose true entry (the previous lane's exit - SB) differs re-walks
+         * from it until it meets a start of its own walk (the paths coincide from there) or
+         * leaves the segment (its exit changed: the next lane re-checks) */
+        const uint64_t ts0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+        for (;;) {
+            const uint32_t pe = dpp_prev(exit); /* all lanes active: a DPP read of a lane outside exec yields 0 */
+            const uint32_t te = lane ? pe - SB : e0;
+            const bool redo = te != ent;
+            if (!any_lane(redo)) break;
+            pw_stat(r, stats, 1);
+            if (redo) {
+                if (te >= SB) { /* the previous lane's last codeword covers this segment */
+#pragma unroll
+                    for (int j = 0; j < SW; j++) m[j] = 0u;
+                    exit = te;
+                    slow = false;
+                } else {
+                    uint32_t nm[SW];
+                    bool s2, mg;
+                    const uint32_t pos = seg_walk<SW, true>(w, te, k1, nsteps, m, nm, s2, mg);
+                    if (mg) { /* merged at pos: the old starts from pos on, its exit and slow flag hold */
+#pragma unroll
+                        for (int j = 0; j < SW; j++) {
+                            const uint32_t lo = 32u * (uint32_t)j;
+                            const uint32_t keep = pos <= lo ? ~0u : (pos >= lo + 32u ? 0u : (~0u << (pos - lo)));
+                            m[j] = nm[j] | (m[j] & keep);
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < SW; j++) m[j] = nm[j];
+                        exit = s2 ? SB : pos;
+                        slow = s2;
+                    }
+                }
+                ent = te;
+            }
+        }
+        if (stats) pw_stat(r, true, 7, __builtin_amdgcn_s_memtime() - ts0);
+        /* 3. count */
+        uint32_t n = 0;
+#pragma unroll
+        for (int j = 0; j < SW; j++) n += (uint32_t)__builtin_popcount(m[j]);
+        const uint32_t incl = wave_incl_scan(n);
+        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        const uint32_t L = total >= cnt ? wr_u((uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(incl >= cnt))) : 63u;
+        /* a slow lane at or before the last lane that matters: measure this partition serially */
+        if (__builtin_amdgcn_ballot_w64(slow && lane <= L)) {
+            pw_stat(r, stats, 2);
+            return wave_rice_skip_serial(r, cnt, k, limit);
+        }
+        if (total < cnt) {
+            cnt -= total;
+            r.pos = ((uint64_t)(ws + SW * 63u) << 5) + __builtin_amdgcn_readlane(exit, 63);
+            continue;
+        }
+        /* the lane holding codeword #cnt; its end is the next codeword start */
+        uint32_t endpos = exit;
+        if (lane == L) {
+            uint32_t j = cnt - (incl - n) + 1u; /* 1-based index of the start after the partition's last codeword */
+            bool found = false;
+#pragma unroll
+            for (int t = 0; t < SW; t++) {
+                const uint32_t c = (uint32_t)__builtin_popcount(m[t]);
+                if (!found && j <= c) {
+                    uint32_t mm = m[t];
+                    for (uint32_t d = j; d > 1u; d--) mm &= mm - 1u;
+                    endpos = 32u * (uint32_t)t + (uint32_t)__builtin_ctz(mm);
+                    found = true;
+                }
+                if (!found) j -= c;
+            }
+        }
+        r.pos = ((uint64_t)(ws + SW * L) << 5) + __builtin_amdgcn_readlane(endpos, L);
+        cnt = 0;
+    }
+    return true;
+}
+/* skip_residual for the wave-uniform reader: partition headers read at the uniform cursor,
+ * each partition's codewords skipped by the wave scan (same TRUNC/OK outcomes as the lane walk) */
+/* Pass width for a partition: lane segments of SW words, so that one pass of 64 lanes (2048 SW
+ * bits) covers about the whole partition -- a short partition (C2: ~2,600 bits) would waste a
+ * wide pass, a long one (C5: ~60,000 bits) would pay per-pass overheads many times.  seg > 0
+ * forces a width (BNFLAC_PW_SEG, experiments). */
+DEV bool wave_rice_skip_any(WR &r, uint32_t cnt, uint32_t k, uint64_t limit, bool stats, int seg) {
+    const uint32_t est = cnt * (k + 2u); /* bits, at about one unary zero per codeword */
+    const int sw = seg > 0 ? seg : est > 6u * 2048u ? 16 : est > 3u * 2048u ? 8 : est > 3u * 1024u ? 4 : est > 1536u ? 2 : 1;
+    switch (sw) {
+    case 1: return wave_rice_skip<1>(r, cnt, k, limit, stats);
+    case 2: return wave_rice_skip<2>(r, cnt, k, limit, stats);
+    case 4: return wave_rice_skip<4>(r, cnt, k, limit, stats);
+    case 8: return wave_rice_skip<8>(r, cnt, k, limit, stats);
+    default: return wave_rice_skip<16>(r, cnt, k, limit, stats);
+    }
+}
+DEV uint32_t wave_skip_residual(WR &r, const SubHdr &h, uint32_t bs, uint64_t limit, bool stats, int seg) {
+    const uint32_t parts = 1u << h.porder;
+    const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
+    const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
+    for (uint32_t p = 0; p < parts; p++) {
+        if (br_pos(r) > limit) return BNF_ST_TRUNC; /* the previous partition ended past the buffer */
+        const uint32_t kk = wr_u(br_read(r, plen));
+        const uint32_t cnt = (h.porder == 0 || p > 0) ? psamples : psamples - h.order;
+        if (kk >= pesc) {
+            const uint32_t nb = wr_u(br_read(r, 5));
+            r.pos += (uint64_t)nb * cnt;
+        } else if (cnt && !wave_rice_skip_any(r, cnt, kk, limit, stats, seg)) {
+            return BNF_ST_TRUNC;
+        }
+    }
+    return br_pos(r) > limit ? BNF_ST_TRUNC : BNF_ST_OK;
 }
 
 #if BNF_TU == 0
@@ -1273,6 +1613,104 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     const uint32_t lanec = crc16_shift(1u, 16u * (63u - lane));
     __syncthreads();
     crc_frames((const uint8_t *)words, nbytes, frame_offs, nframes, (b - pb) * CRC_FPW, info, T, TK, lanec, lane);
+}
+
+/* =========================================================== k_parse_wave
+ * One wave per frame: the same record as parse_frame (header, subframe starts, decode class),
+ * with the header and subframe headers read at a wave-uniform cursor (WR) and each Rice
+ * partition of subframes 0..C-2 crossed by the wave-cooperative scan (wave_rice_skip).
+ * For launches with few frames (C5's files, one stream in the reader) the lane-per-frame walk
+ * is one lane's serial chain over C-1 subframes with ~59 waves on 256 CUs; here every frame
+ * has a wave of its own.  Identical records are a tested property (tests/test_gpu_parse_wave.py). */
+__global__ void __launch_bounds__(64) k_parse_wave(const uint32_t *__restrict__ words, uint64_t nbytes,
+                                                   const uint64_t *__restrict__ frame_offs, uint32_t nframes,
+                                                   bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
+                                                   uint64_t base_sample, bnf_frame_info *__restrict__ info,
+                                                   uint32_t stats, int seg) {
+    __shared__ LDS_DMA_ALIGN uint32_t ring[WR_SLOTS * WR_WIN];
+    const uint32_t lane = threadIdx.x, f = blockIdx.x;
+    if (f >= nframes) return;
+    bnf_frame_info fi;
+    fi.status = BNF_ST_OK;
+    fi.err = -1;
+    fi.frame_off = frame_offs[f];
+    fi.resume_bit = 0;
+    fi.cached = -1;
+    fi.blocksize = fi.sample_rate = fi.channels = fi.assignment = fi.bps = 0;
+    fi.number_type = 0;
+    fi.unparseable = 0;
+    fi.number = 0;
+    fi.out_sample = 0;
+    fi.crc8 = fi.crc16_calc = fi.crc16_read = fi.crc_ok = 0;
+    fi.flags = 0;
+    fi.crc_next = 0;
+    uint32_t ss[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) ss[c] = 0;
+    const uint64_t limit = nbytes * 8u;
+    const uint64_t fbit = fi.frame_off * 8u;
+    WR r;
+    wr_init(r, words, nbytes, (lds_u32 *)ring, fbit);
+    pw_stat(r, stats != 0u, 4);
+    uint32_t st = parse_header(r, fbit, limit, sp, fi);
+    if (st == BNF_ST_ERROR && br_pos(r) > limit) st = BNF_ST_TRUNC;
+    if (st == BNF_ST_OK) {
+        uint64_t sample;
+        if (fi.number_type == 1) sample = fi.number;
+        else if (sp.has_stream_info && sp.min_blocksize == sp.max_blocksize) sample = (uint64_t)sp.min_blocksize * fi.number;
+        else sample = (uint64_t)fi.blocksize * fi.number;
+        fi.out_sample = out_sample_in ? out_sample_in[f] : sample - base_sample;
+        uint32_t maxorder = 0;
+        bool raw = false;
+        const uint32_t nch = wr_u(fi.channels), bs = wr_u(fi.blocksize);
+        for (uint32_t ch = 0; ch < nch; ch++) {
+            const uint32_t here = (uint32_t)(br_pos(r) - fbit);
+#pragma unroll
+            for (int c = 0; c < 8; c++) ss[c] = (uint32_t)c == ch ? here : ss[c];
+            if (ch + 1 == nch) {
+                const uint32_t x = br_peek(r) >> 24;
+                if (!(x & 0x80u) && (x & 0x7Eu) >= 0x40u) maxorder = max(maxorder, ((x >> 1) & 31u) + 1u);
+                raw = raw || (x & 0x7Eu) < 4u;
+                break;
+            }
+            SubHdr h;
+            int32_t err = -1;
+            st = parse_subframe_head<false>(r, sub_bps(fi, ch), bs, limit, h, nullptr, nullptr, err);
+            if (st == BNF_ST_OK) {
+                if (h.type == T_LPC) maxorder = max(maxorder, h.order);
+                raw = raw || h.type == T_CONST || h.type == T_VERB;
+                if (h.type == T_VERB) br_skip(r, (uint64_t)h.bps * bs);
+                else if (h.type == T_FIXED || h.type == T_LPC) {
+                    const uint64_t t0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+                    st = wave_skip_residual(r, h, bs, limit, stats != 0u, seg);
+                    if (stats) pw_stat(r, true, 5, __builtin_amdgcn_s_memtime() - t0);
+                }
+                if (st == BNF_ST_OK && br_pos(r) > limit) st = BNF_ST_TRUNC;
+            }
+            if (st == BNF_ST_ERROR && br_pos(r) > limit) st = BNF_ST_TRUNC;
+            if (st != BNF_ST_OK) {
+                if (st == BNF_ST_ERROR) {
+                    fi.err = err;
+                    fi.resume_bit = br_pos(r);
+                }
+                break;
+            }
+        }
+        if (maxorder > 16) fi.flags |= BNF_FL_W32;
+        else if (maxorder > 8 || (maxorder > 0 && fi.bps > 16)) fi.flags |= BNF_FL_W16;
+        else if (fi.channels == 2 && fi.bps <= 16 && !raw) fi.flags |= BNF_FL_ST;
+    }
+    fi.status = st;
+#pragma unroll
+    for (int c = 0; c < 8; c++) fi.sub_start[c] = ss[c];
+    wait_vm(); /* no DMA may land in the ring after the wave is gone */
+    pw_flush(r, stats != 0u);
+    /* the record, one dword per lane (32 lanes, one store) */
+    const uint32_t *src = (const uint32_t *)&fi;
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) v = lane == (uint32_t)i ? src[i] : v;
+    if (lane < 32u) ((uint32_t *)&info[f])[lane] = v;
 }
 
 /* The same CRC pass as its own kernel, for a second stream: it runs beside k_parse and the
@@ -3170,7 +3608,33 @@ static SideQ *side_queue() { /* under g_side_mu; nullptr: decode serially */
     return &q;
 }
 
+/* Parse kernel choice: k_parse_wave (a wave per frame) for launches too small to fill the
+ * chip with lane-per-frame waves, k_parse otherwise.  BNFLAC_PARSE_WAVE=0 never, 1 always.
+ * Default, from tools/pw_stats.py on one box (lane walk vs wave scan, ms): C2 1,024 frames
+ * 0.47 vs 0.12, 4,096 0.47 vs 0.21, 16,384 0.47 vs 0.62; C3 8,192 0.94 vs 0.19; C5 469 3.53 vs
+ * 0.32, 3,752 3.33 vs 0.53; C4 4,096 2.56 vs 1.69.  The lane walk only wins once there are
+ * ~256 lane-waves of short-partition frames: wave up to 8,192 frames, and up to 32,768 for
+ * streams whose subframes are long (above 16 bits or more than 2 channels). */
+static int g_parse_wave = -1;
+static bool use_parse_wave(uint32_t nframes, const bnf_stream_params &sp) {
+    if (g_parse_wave < 0) {
+        const char *e = getenv("BNFLAC_PARSE_WAVE");
+        g_parse_wave = e ? (atoi(e) ? 1 : 0) : 2;
+    }
+    if (g_parse_wave != 2) return g_parse_wave == 1;
+    return nframes <= 8192u || (nframes <= 32768u && (sp.bps > 16u || sp.channels > 2u));
+}
+
 extern "C" {
+void bnf_set_parse_wave(int mode) { g_parse_wave = mode < 0 ? 2 : (mode ? 1 : 0); } /* -1: auto */
+hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset) { /* debug counters of k_parse_wave (BNFLAC_PW_STATS=1) */
+    hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_pw_stats), 8 * sizeof(uint64_t));
+    if (e == hipSuccess && reset) {
+        static const uint64_t z[8] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_pw_stats), z, sizeof z);
+    }
+    return e;
+}
 /* crc: 0 none; 1 the CRC pass inside k_parse's launch; 2 k_crc on `side`, forked from s
  * (ev_fork) and finished at ev_crc, for bnf_launch_decode's deferred check */
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
@@ -3186,6 +3650,13 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
                            nframes, info);
         e = hipEventRecord(ev_crc, side);
         if (e != hipSuccess) return e;
+    }
+    if (crc == 0 && use_parse_wave(nframes, sp)) {
+        static const uint32_t pws = getenv("BNFLAC_PW_STATS") ? 1u : 0u;
+        static const int seg = [] { const char *e = getenv("BNFLAC_PW_SEG"); return e ? atoi(e) : 0; }();
+        hipLaunchKernelGGL(k_parse_wave, dim3(nframes), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
+                           out_sample_in, base_sample, info, pws, seg);
+        return hipGetLastError();
     }
     const uint32_t *perm = nullptr;
     if (order) {

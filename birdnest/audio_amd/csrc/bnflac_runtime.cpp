@@ -148,6 +148,15 @@ static int crc_pass() { /* 0 off, 1 inside k_parse's launch, 2 concurrent (k_crc
     return g_crc_pass;
 }
 extern "C" BNFLAC_API void bnflac_debug_set_crc_pass(int on) { g_crc_pass = std::min(std::max(on, 0), 2); }
+extern "C" void bnf_set_parse_wave(int mode);
+/* parse kernel: -1 auto (k_parse_wave for small launches), 0 k_parse, 1 k_parse_wave (tests, A/B) */
+extern "C" BNFLAC_API void bnflac_debug_set_parse_wave(int mode) { bnf_set_parse_wave(mode); }
+extern "C" hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset);
+/* k_parse_wave's debug counters (collected when BNFLAC_PW_STATS is set): passes, splice rounds,
+ * serial fallbacks, partitions, frames, wave-cycles in scans.  out8: 8 values. */
+extern "C" BNFLAC_API int bnflac_debug_parse_wave_stats(uint64_t *out8, int reset) {
+    return bnf_parse_wave_stats(out8, reset) == hipSuccess ? 0 : -1;
+}
 extern "C" BNFLAC_API int bnflac_debug_stats(uint64_t *out16, int reset) {
     return bnf_stats(out16, reset) == hipSuccess ? 0 : fail("bnflac_debug_stats failed");
 }

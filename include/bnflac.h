@@ -183,6 +183,13 @@ BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags);
  * and the decode of the same records (bnflac_decode_parsed then finishes the check).
  * Default 0 (env BNFLAC_CRC_PASS=1|2). */
 BNFLAC_API void bnflac_debug_set_crc_pass(int on);
+/* Development / test switch: parse kernel (-1 auto, 0 lane-per-frame k_parse, 1 wave-per-frame
+ * k_parse_wave); both write identical records. */
+BNFLAC_API void bnflac_debug_set_parse_wave(int mode);
+/* Debug: k_parse_wave's counters, collected while BNFLAC_PW_STATS is set in the environment
+ * (passes, splice rounds, serial fallbacks, partitions, frames, scan / window-wait / splice
+ * wave-cycles).  out8 holds 8 values; reset != 0 clears them.  0 or -1. */
+BNFLAC_API int bnflac_debug_parse_wave_stats(uint64_t *out8, int reset);
 /* Debug: k_decode event counters collected while ablate bit 0x100 is set: [0..5] fused
  * chunks, generic chunks, DMA landing waits, slow Rice codewords, refills, waves (wave-level
  * events); [8..12] shader-clock cycles summed over waves in setup, chunk decode, refill,
