@@ -2577,6 +2577,9 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  * mismatch, out-of-range samples, unsupported layouts) get BNF_FL_REDO and are decoded
  * again, exactly, by k_decode<8>, which runs after it on the same stream. */
 #define ST_CHK 16 /* samples per chunk (one 64-byte FLACDecoder run per frame) */
+#ifndef BNF_ST_PAIR
+#define BNF_ST_PAIR 1 /* fused chunks decode Rice codewords two per window (st_fused_pair) */
+#endif
 #define ST_RD 8  /* 16-byte ring slots per lane and channel: two 64-byte groups */
 
 struct StCh {
@@ -3038,6 +3041,121 @@ DEV void st_fused_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
     }
 }
 
+/* The restore and output half of st_fused_step for sample T of both channels, given the
+ * folded Rice values u0 / u1 (zig-zag applied here). */
+template <int T, int FMT>
+DEV void st_lpc_out(StCh &z0, StCh &z1, uint32_t u0, uint32_t u1, int32_t (&L)[4], int32_t (&R)[4], bool as_uni,
+                    uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al, uint32_t bs, bool store,
+                    u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1, bool anyw) {
+    constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
+    int32_t p0, p1, n0, n1;
+    st_fin2(z0, z1, z0.q[(T + 7) & 7], z1.q[(T + 7) & 7], pre0, pre1, p0, p1); /* this sample's prediction */
+    st_pre2<T>(z0, z1, n0, n1);                                                /* the next one's older taps */
+    pre0 = n0;
+    pre1 = n1;
+    const int32_t s0 = (int32_t)(((u0 >> 1) ^ (0u - (u0 & 1u))) + (uint32_t)(p0 >> z0.sh));
+    const int32_t s1 = (int32_t)(((u1 >> 1) ^ (0u - (u1 & 1u))) + (uint32_t)(p1 >> z1.sh));
+    if (T & 1) {
+        st_range(z0, L[(T + 3) & 3], s0);
+        st_range(z1, R[(T + 3) & 3], s1);
+    }
+    z0.q[T] = __builtin_amdgcn_perm(z0.q[(T + 7) & 7], (uint32_t)s0, 0x05040100u);
+    z1.q[T] = __builtin_amdgcn_perm(z1.q[(T + 7) & 7], (uint32_t)s1, 0x05040100u);
+    L[T & 3] = s0;
+    R[T & 3] = s1;
+    if ((T & 3) == 3) {
+        if (__builtin_expect(anyw, 0)) { /* wasted bits (wave-uniform test) */
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                L[q] = (int32_t)((uint32_t)L[q] << z0.wasted);
+                R[q] = (int32_t)((uint32_t)R[q] << z1.wasted);
+            }
+        }
+        st_decor4(as_uni, as_u, as, L, R);
+        if (STG) {
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_perm((uint32_t)R[q], (uint32_t)L[q], 0x05040100u);
+            pk[T >> 2] = u32x4{w[0], w[1], w[2], w[3]};
+        } else if (store) {
+            st_emit4<FMT>(dst, nbase + (uint32_t)T - 3u, 4u, al, bs, L, R);
+        }
+    }
+}
+
+/* Two Rice codewords of one channel from one 32-bit window (the pair fits when their lengths
+ * sum to <= 32: always at C2's parameters, k = 8 and ~10-bit codewords).  The second's prefix
+ * is counted in the window shifted past the first; ffbh of an all-zero window is clamped to
+ * 32 so a prefix that runs off the window always reads as not fitting.  Returns the bits
+ * both take, or 0 with sl set (the lane then decodes the two with the generic reader). */
+DEV uint32_t st_rice_pair(const StCh &z, uint32_t &ua, uint32_t &ub, bool &sl) {
+    const uint32_t w = br_peek(z.b);
+    const uint32_t qa = min(ffbh(w), 32u);
+    const uint32_t la = qa + z.k1;
+    const uint32_t w2 = w << (la & 31u); /* la == 32: garbage, and n > 32 below */
+    const uint32_t qb = min(ffbh(w2), 32u);
+    ua = (qa << z.k) | __builtin_amdgcn_ubfe(w, z.km - qa, z.k);
+    ub = (qb << z.k) | __builtin_amdgcn_ubfe(w2, z.km - qb, z.k);
+    const uint32_t n = la + qb + z.k1;
+    sl = n > 32u;
+    return sl ? 0u : n;
+}
+/* rare cases of a pair step, per channel: the ring words past the landed ones, or a pair that
+ * does not fit the window (both codewords through the generic reader) */
+DEV void st_rare_pair(StCh &z, bool sl, bool ld, uint32_t &ua, uint32_t &ub, uint64_t limit, uint32_t &trunc,
+                      uint32_t nst, uint32_t lane) {
+    if (any_lane(ld)) {
+        st_land(z.b, nst);
+        if (z.b.wi + 1u >= z.b.vendw) {
+            wait_vm();
+            br_refill(z.b);
+            wait_vm();
+            br_drained(z.b);
+        }
+        st_next_word(z.b);
+    }
+    if (any_lane(sl)) {
+        STAT(z.b.stats, 3);
+        if (sl) {
+            uint32_t qq;
+            if (!br_unary(z.b, qq, limit)) trunc = 1;
+            ua = (qq << z.k) | br_read(z.b, z.k);
+            if (!br_unary(z.b, qq, limit)) trunc = 1;
+            ub = (qq << z.k) | br_read(z.b, z.k);
+        }
+    }
+    st_resync(z.b, lane);
+}
+/* Samples T and T + 1 (T even) of both channels: one window peek, one cursor advance and one
+ * ring read per channel for two codewords (st_fused_step does one of each per codeword), then
+ * the two restores in order. */
+template <int T, int FMT>
+DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
+                       uint32_t nq, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al,
+                       uint32_t bs, bool store, u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1,
+                       uint32_t lane, bool anyw) {
+    static_assert((T & 1) == 0, "pairs start on even samples");
+    constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
+    constexpr uint32_t spg = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u;
+    const uint32_t nqt = nq + ((!STG && T >= 4 && store) ? spg : 0u); /* + this group's direct store */
+    uint32_t u0a, u0b, u1a, u1b;
+    bool sl0, sl1;
+    const uint32_t n0 = st_rice_pair(z0, u0a, u0b, sl0), n1 = st_rice_pair(z1, u1a, u1b, sl1);
+    const uint32_t laneb = lane << 4;
+    st_adv_nc(z0.b, n0, laneb);
+    st_adv_nc(z1.b, n1, laneb);
+    /* the word read now and the one the next pair may read must have landed */
+    const bool ld0 = z0.b.wi >= z0.b.vlim, ld1 = z1.b.wi >= z1.b.vlim;
+    st_next_word(z0.b);
+    st_next_word(z1.b);
+    if (__builtin_expect(any_lane(sl0 || sl1 || ld0 || ld1), 0)) {
+        st_rare_pair(z0, sl0, ld0, u0a, u0b, limit, trunc, nqt, lane);
+        st_rare_pair(z1, sl1, ld1, u1a, u1b, limit, trunc, nqt, lane);
+    }
+    st_lpc_out<T, FMT>(z0, z1, u0a, u1a, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
+    st_lpc_out<T + 1, FMT>(z0, z1, u0b, u1b, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
+}
+
 /* One sample of both channels on the general path: warm-up, partition headers anywhere,
  * escaped partitions, the frame's last partial chunk.  Returns whether a store was issued. */
 template <int T, int FMT>
@@ -3166,9 +3284,15 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                     const uint32_t nq = nst + (STG ? 0u : g * 2u * ST_SPG); /* stores issued since the DMAs (at least) */
                     const uint32_t nb = n0 + g * 8u;
                     const bool sto = !(ablate & 2u);
+#if BNF_ST_PAIR
+#define FPAIR(T) st_fused_pair<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
+                    FPAIR(0); FPAIR(2); FPAIR(4); FPAIR(6);
+#undef FPAIR
+#else
 #define FSTEP(T) st_fused_step<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
                     FSTEP(0); FSTEP(1); FSTEP(2); FSTEP(3); FSTEP(4); FSTEP(5); FSTEP(6); FSTEP(7);
 #undef FSTEP
+#endif
                     if (STG && g == 0) { pk01[0] = pk[0]; pk01[1] = pk[1]; }
                 }
                 z0.left -= ST_CHK;
