@@ -1967,15 +1967,13 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
         else FN<CHK, MAXW, P_WIDE>(__VA_ARGS__);                                                   \
     } while (0)
 
+/* one block of fpb decode-order slots (the body of k_decode) */
 template <int MAXW, int CHK, int RD>
-__global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
-                                                      uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
-                                                      int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
-                                                      bnf_frame_info *__restrict__ info,
-                                                      const uint32_t *__restrict__ perm, uint32_t ablate) {
+DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t *__restrict__ words, uint64_t nbytes,
+                      uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *__restrict__ out,
+                      uint64_t out_bytes, bnf_frame_info *__restrict__ info, const uint32_t *__restrict__ perm,
+                      uint32_t ablate) {
     static_assert(MAXW <= CHK && CHK % 8 == 0 && RD <= RING_MAX, "chunk must hold the predictor ring");
-    __shared__ LDS_DMA_ALIGN uint32_t ring[RD * RING_LANE_DW];
-    __shared__ int32_t lds[CHK * RP]; /* [sample][lane] */
     static_assert(CHK * RP >= 1024 + 512, "row buffer also holds the CRC tables and the tail's frame table");
     /* per-frame tables overlay the buffers while those are idle: the setup exchange uses
      * the ring before its first DMA, the tail uses the row buffer after the last pack */
@@ -1991,7 +1989,7 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
     const uint32_t fl = lane >> lg, ch = lane & (chn_lanes - 1u);
     /* frame of this lane group: slot order, or the decode order k_order built (class, then
      * blocksize: similar frames share a wave) */
-    const uint32_t slot = blockIdx.x * fpb + fl;
+    const uint32_t slot = blk * fpb + fl;
     const uint32_t f = (perm && fl < fpb && slot < nframes) ? perm[slot] : slot;
     const uint64_t limit = nbytes * 8u;
 
@@ -2000,6 +1998,13 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
     if (MAXW != 8) { /* most blocks are not this instance's: leave on two words of the record */
         const bool w = have && info[f].status == BNF_ST_OK && (info[f].flags & (BNF_FL_W16 | BNF_FL_W32)) &&
                        !(info[f].flags & BNF_FL_ST);
+        if (!__any(w)) return;
+    } else { /* W = 8: narrow non-stereo frames, and stereo frames k_decode_st handed back */
+        bool w = false;
+        if (have && info[f].status == BNF_ST_OK) {
+            const uint32_t fl = info[f].flags;
+            w = ((fl & BNF_FL_ST) && !(ablate & 0x400u)) ? (fl & BNF_FL_REDO) != 0 : !(fl & (BNF_FL_W16 | BNF_FL_W32));
+        }
         if (!__any(w)) return;
     }
     if (have) fi = info[f];
@@ -2371,6 +2376,33 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
         }
         for (uint64_t i = lane; i < nbytes_fr; i += DEC_LANES) out[start + i] = 0;
     }
+    wait_vm(); /* no ring DMA may land after the wave is gone */
+}
+
+/* The W instances, one block of decode-order slots per workgroup.  seg (W = 16 / 32, with
+ * perm): the decode order's bucket ends (k_order_place leaves seg[k] = end of bucket k), so
+ * a block outside the instance's class segment leaves on two scalar loads, before reading
+ * any frame record (C2: all 32,768 blocks of each side launch).  A persistent grid over the
+ * segment (workgroups claiming blocks from a counter) removed those waves altogether but
+ * compiled the block body ~7% slower inside the loop (C3 13.1 -> 13.9 ms, C4 27.7 -> 29.6;
+ * same with a full-size grid), for no C2 gain (12.33 -> 12.30 ms): DESIGN.md section 9. */
+template <int MAXW, int CHK, int RD>
+__global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restrict__ words, uint64_t nbytes,
+                                                      uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
+                                                      int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
+                                                      bnf_frame_info *__restrict__ info,
+                                                      const uint32_t *__restrict__ perm, uint32_t ablate,
+                                                      const uint32_t *__restrict__ seg) {
+    __shared__ LDS_DMA_ALIGN uint32_t ring[RD * RING_LANE_DW];
+    __shared__ int32_t lds[CHK * RP]; /* [sample][lane] */
+    if (MAXW != 8 && seg) {
+        const uint32_t fpb = DEC_LANES >> __builtin_ctz(chn_lanes);
+        const uint32_t c = MAXW == 32 ? 3u : 2u; /* order_key's class */
+        const uint32_t lo = seg[c * 64u - 1u] / fpb, end = (seg[c * 64u + 63u] + fpb - 1u) / fpb;
+        if (blockIdx.x < lo || blockIdx.x >= end) return;
+    }
+    decode_block<MAXW, CHK, RD>(blockIdx.x, ring, lds, words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info,
+                                perm, ablate);
 }
 
 #if BNF_TU == 0
@@ -2577,6 +2609,13 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  * mismatch, out-of-range samples, unsupported layouts) get BNF_FL_REDO and are decoded
  * again, exactly, by k_decode<8>, which runs after it on the same stream. */
 #define ST_CHK 16 /* samples per chunk (one 64-byte FLACDecoder run per frame) */
+/* CRC-16 from the rings while decoding (measured alternative, off: see below and DESIGN.md
+ * section 9): 1 steps once per chunk, 2 inside the fused pairs.  0: the frame's bytes are
+ * read again after the decode (st_crc16). */
+#ifndef BNF_ST_RING_CRC
+#define BNF_ST_RING_CRC 0
+#endif
+#define BNF_ST_CRC_PAIRS (BNF_ST_RING_CRC == 2)
 #ifndef BNF_ST_PAIR
 #define BNF_ST_PAIR 1 /* fused chunks decode Rice codewords two per window (st_fused_pair) */
 #endif
@@ -2591,6 +2630,7 @@ struct StCh {
     uint32_t esc, left, pidx, nparts, psamples, plen, pesc, porder, order;
     uint32_t wasted;
     int32_t lim, mx, mn; /* operand range of the path, sample range seen */
+    uint32_t crc, ca, ce; /* in-ring CRC-16: running value, next byte, end of the channel's range (absolute, mod 2^32) */
 };
 
 /* lo | hi << 16 from the low halves */
@@ -2845,6 +2885,9 @@ DEV void st_refill_issue(BR &b, bool want) {
 DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line offset o: bytes below h cleared */
     return h <= o ? ~0u : (h >= o + 4u ? 0u : (~0u << (8u * (h - o))));
 }
+#ifndef CRC_LINES
+#define CRC_LINES 4
+#endif
 DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
     const lds_u16 *Tb = T + CRC11_BYTE;
     uint32_t crc = 0;
@@ -2855,28 +2898,35 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
     const uint32_t nl = b1 > p0 ? (uint32_t)((b1 - p0) >> 6) : 0u;
     uint64_t p = b0;
     if (nl) {
+        /* CRC_LINES lines in flight per lane: each lane walks its own frame, so the loads of
+         * one line wait a full HBM latency; one line ahead left the loop latency-bound */
         const uint4 *q = (const uint4 *)(bytes + p0);
-        uint4 cur[4], nxt[4];
+        uint4 buf[CRC_LINES][4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) cur[u] = q[u];
+        for (int d = 0; d < CRC_LINES; d++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) buf[d][u] = q[4u * min((uint32_t)d, nl - 1u) + u];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            cur[u].x &= st_hmask(h, 16u * u);
-            cur[u].y &= st_hmask(h, 16u * u + 4u);
-            cur[u].z &= st_hmask(h, 16u * u + 8u);
-            cur[u].w &= st_hmask(h, 16u * u + 12u);
+            buf[0][u].x &= st_hmask(h, 16u * u);
+            buf[0][u].y &= st_hmask(h, 16u * u + 4u);
+            buf[0][u].z &= st_hmask(h, 16u * u + 8u);
+            buf[0][u].w &= st_hmask(h, 16u * u + 12u);
         }
-        for (uint32_t i = 0; i < nl; i++) {
-            const uint32_t j = min(i + 1u, nl - 1u);
+        for (uint32_t i = 0; i < nl; i += CRC_LINES) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) nxt[u] = q[4u * j + u];
+            for (int d = 0; d < CRC_LINES; d++) {
+                if (i + d < nl) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                crc = crc16_step8w(crc, __builtin_bswap32(cur[u].x), __builtin_bswap32(cur[u].y), T);
-                crc = crc16_step8w(crc, __builtin_bswap32(cur[u].z), __builtin_bswap32(cur[u].w), T);
+                    for (int u = 0; u < 4; u++) {
+                        crc = crc16_step8w(crc, __builtin_bswap32(buf[d][u].x), __builtin_bswap32(buf[d][u].y), T);
+                        crc = crc16_step8w(crc, __builtin_bswap32(buf[d][u].z), __builtin_bswap32(buf[d][u].w), T);
+                    }
+                    const uint32_t j = min(i + d + CRC_LINES, nl - 1u);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) buf[d][u] = q[4u * j + u];
+                }
             }
-#pragma unroll
-            for (int u = 0; u < 4; u++) cur[u] = nxt[u];
         }
         p = p0 + (uint64_t)nl * 64u;
         /* the last partial line: whole 8-byte steps (loads issued together), then bytes */
@@ -2892,6 +2942,58 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
     }
     while (p < b1) { crc = ((crc << 8) ^ Tb[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
     return crc;
+}
+
+/* ---- CRC-16 from the rings (read_frame_'s frame CRC, @0x10011a01).  The frame's bytes pass
+ * through the two channel rings as they are decoded: channel 0's cursor walks [frame start,
+ * X) and channel 1's [X, end) (X: the byte of subframe 1's first bit).  Each channel keeps a
+ * running CRC over its range, advanced from the ring in 8-byte steps (slice-by-8 table, 4 KB
+ * in LDS beside the rings) behind its decode cursor: a few steps per chunk, and before a
+ * refill overwrites ring slots every byte in them is folded in.  Bytes the rings never hold
+ * (the frame header, the words the cursor starts on) and the last few bytes go through
+ * global memory; the two ranges are combined by a GF(2) shift (crc16_shift).  Round 2 read
+ * the whole frame again after decoding it: ~11 GB of HBM reads per C2 step. */
+DEV uint32_t crc16_cont_global(uint32_t crc, const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1,
+                               const lds_u16 *T) {
+    uint64_t p = b0;
+    while (p < b1 && (p & 7u)) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xffu]) & 0xffffu; p++; }
+    while (p + 8u <= b1) {
+        const uint2 v = *(const uint2 *)(bytes + p);
+        crc = crc16_step8(crc, __builtin_bswap32(v.x), __builtin_bswap32(v.y), T);
+        p += 8u;
+    }
+    while (p < b1) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xffu]) & 0xffffu; p++; }
+    return crc;
+}
+/* one 8-byte step of channel z's in-ring CRC (on: this lane steps) */
+DEV void st_crc_step(StCh &z, bool on, const lds_u16 *T) {
+    const uint32_t a = z.ca; /* absolute byte, 8-aligned */
+    const uint32_t off = ((a >> 4) & (ST_RD - 1u)) * (RING_LANE_DW * 4u) + (a & 8u);
+    const lds_u32 *q = z.b.lring + (off >> 2);
+    const uint32_t c = crc16_step8(z.crc, __builtin_bswap32(q[0]), __builtin_bswap32(q[1]), T);
+    z.crc = on ? c : z.crc;
+    z.ca += on ? 8u : 0u;
+}
+/* whether the ring still holds byte z.ca: a blocking refill (rare paths: landings, escapes)
+ * may overwrite blocks before the CRC has passed them; those go through global memory */
+DEV bool st_crc_held(const StCh &z) { return (int32_t)(z.ca - ((z.b.iend - ST_RD) << 4)) >= 0; } /* mod 2^32 bytes */
+/* whether channel z's next CRC step is behind its decode cursor, inside its range and held */
+DEV bool st_crc_ready(const StCh &z) {
+    return (int32_t)((uint32_t)(br_pos(z.b) >> 3) - z.ca) >= 8 && (int32_t)(z.ce - z.ca) >= 8 && st_crc_held(z);
+}
+/* rare: a lane whose next CRC byte left the ring continues through global memory up to the
+ * ring's oldest block (or the end of its range) */
+DEV void st_crc_lost(StCh &z, bool on, const uint8_t *bytes, uint64_t frame_off, uint32_t fo, const lds_u16 *T) {
+    if (on && (int32_t)(z.ce - z.ca) > 0 && !st_crc_held(z)) {
+        const uint32_t old = (z.b.iend - ST_RD) << 4;
+        const uint32_t to = (int32_t)(z.ce - old) < 0 ? z.ce : old;
+        z.crc = crc16_cont_global(z.crc, bytes, frame_off + (uint32_t)(z.ca - fo), frame_off + (uint32_t)(to - fo), T);
+        z.ca = to;
+    }
+}
+/* ... and whether it lies before byte b (mod 2^32) */
+DEV bool st_crc_before(const StCh &z, uint32_t b) {
+    return (int32_t)(b - z.ca) >= 8 && (int32_t)(z.ce - z.ca) >= 8 && st_crc_held(z);
 }
 
 /* Fused-path cursor (4-slot ring).  ra is the LDS byte offset of ring word wi inside the
@@ -3133,7 +3235,7 @@ template <int T, int FMT>
 DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
                        uint32_t nq, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al,
                        uint32_t bs, bool store, u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1,
-                       uint32_t lane, bool anyw) {
+                       uint32_t lane, bool anyw, const lds_u16 *CT) {
     static_assert((T & 1) == 0, "pairs start on even samples");
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t spg = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u;
@@ -3154,6 +3256,11 @@ DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
     }
     st_lpc_out<T, FMT>(z0, z1, u0a, u1a, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
     st_lpc_out<T + 1, FMT>(z0, z1, u0b, u1b, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
+#if BNF_ST_CRC_PAIRS
+    /* one in-ring CRC step per pair, channels alternating: independent of the decode chain */
+    StCh &zc = ((T >> 1) & 1) ? z1 : z0;
+    st_crc_step(zc, st_crc_ready(zc), CT);
+#endif
 }
 
 /* One sample of both channels on the general path: warm-up, partition headers anywhere,
@@ -3227,6 +3334,11 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     uint8_t *dst = out + os * stride; /* the frame's first byte (planar: channel 0's) */
     const bool al = (((uintptr_t)dst) & 15u) == 0 && (FMT != BNF_OUT_PLANAR32 || (bs & 3u) == 0);
 
+    /* in-ring CRC: the slice-by-8 CRC-16 table behind the rings (16 KB + 4 KB) */
+    lds_u16 *CT = (lds_u16 *)((lds_u32 *)ring + 2 * ST_RD * RING_LANE_DW);
+    static_assert(2 * ST_RD * RING_LANE_DW + 8 * 256 / 2 <= (int)(sizeof(ring) / 4), "CRC table fits behind the rings");
+    if (BNF_ST_RING_CRC)
+        for (uint32_t i = lane; i < 8u * 256u / 2u; i += 64u) ((lds_u32 *)CT)[i] = ((const uint32_t *)&g_crc16_tab[0][0])[i];
     StCh z0, z1;
     lds_u32 *ring0 = (lds_u32 *)ring, *ring1 = (lds_u32 *)ring + ST_RD * RING_LANE_DW;
     br_init(z0.b, words, nbytes, ring0, lane, ST_RD);
@@ -3237,8 +3349,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     const uint64_t t_start = tnow(tmon);
     uint64_t tm_dec = 0, tm_ref = 0, tm_pack = 0;
     if (ok) {
-        const uint64_t fbit = fi.frame_off * 8u;
-        br_seek(z0.b, fbit + fi.sub_start[0]);
+        br_seek(z0.b, fi.frame_off * 8u + fi.sub_start[0]);
         ok = st_setup(z0, sub_bps(fi, 0), bs, limit);
     }
     if (ok) {
@@ -3257,6 +3368,28 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     const uint32_t nchunks = (mybs + ST_CHK - 1) / ST_CHK;
     uint32_t trunc = 0;
     wait_vm(); /* setup loads done: the store count starts from zero */
+    if (BNF_ST_RING_CRC) lds_sync(); /* the CRC table is in LDS */
+    /* in-ring CRC setup: each channel's range up to the oldest ring byte (8-aligned) through
+     * global memory, the rest from the ring */
+    const uint64_t fbit = fi.frame_off * 8u;
+    const uint32_t fo = (uint32_t)fi.frame_off;
+    const bool crc_ring = BNF_ST_RING_CRC && ok && !(ablate & (1u | BNF_MODE_DEFER_CRC));
+    const uint64_t xabs = ok ? (fbit + fi.sub_start[1]) >> 3 : 0ull;
+    z0.crc = z1.crc = 0u;
+    z0.ca = z1.ca = z0.ce = z1.ce = 0u; /* ce == ca: no steps */
+    if (BNF_ST_RING_CRC && crc_ring) {
+        const uint8_t *bytes = (const uint8_t *)words;
+        const uint64_t o0 = max((uint64_t)(z0.b.iend - ST_RD) * 16u, (fi.frame_off + 7u) & ~(uint64_t)7u);
+        const uint64_t s0 = min(o0, xabs);
+        z0.crc = crc16_cont_global(0u, bytes, fi.frame_off, s0, CT);
+        z0.ca = (uint32_t)s0;
+        z0.ce = (uint32_t)xabs;
+        const uint64_t s1 = max((uint64_t)(z1.b.iend - ST_RD) * 16u, (xabs + 7u) & ~(uint64_t)7u);
+        z1.crc = crc16_cont_global(0u, bytes, xabs, s1, CT);
+        z1.ca = (uint32_t)s1;
+        z1.ce = z1.ca + 0x40000000u;
+        wait_vm();
+    }
     uint32_t nst = 0; /* vector-memory ops (PCM stores) issued by this wave since the last refill's DMAs */
     const uint64_t t_loop = tnow(tmon);
     for (uint32_t kc = 0; kc < nchunks; kc++) {
@@ -3285,7 +3418,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                     const uint32_t nb = n0 + g * 8u;
                     const bool sto = !(ablate & 2u);
 #if BNF_ST_PAIR
-#define FPAIR(T) st_fused_pair<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
+#define FPAIR(T) st_fused_pair<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw, CT)
                     FPAIR(0); FPAIR(2); FPAIR(4); FPAIR(6);
 #undef FPAIR
 #else
@@ -3324,6 +3457,30 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
          * stays in flight), then issue the next blocks; the flush's stores are younger */
         {
             const bool want = valid && n0 + ST_CHK < bs;
+            if (BNF_ST_RING_CRC && any_lane(crc_ring)) { /* in-ring CRC: the fused pairs step it; here bytes a blocking refill took, the
+                                       * rest of a general chunk, then the slots this refill overwrites */
+                if (__builtin_expect(any_lane(crc_ring && !(st_crc_held(z0) && st_crc_held(z1))), 0)) {
+                    st_crc_lost(z0, crc_ring, (const uint8_t *)words, fi.frame_off, fo, CT);
+                    st_crc_lost(z1, crc_ring, (const uint8_t *)words, fi.frame_off, fo, CT);
+                }
+#pragma unroll
+                for (int t = 0; t < 3; t++) {
+                    const bool c0 = st_crc_ready(z0), c1 = st_crc_ready(z1);
+                    if (!any_lane(c0 || c1)) break;
+                    st_crc_step(z0, c0, CT);
+                    st_crc_step(z1, c1, CT);
+                }
+                const uint32_t g0 = ((z0.b.wi >> 2) & ~3u) + 4u, g1 = ((z1.b.wi >> 2) & ~3u) + 4u;
+                /* a refilling lane's old group [iend - 8, iend - 4) blocks must be folded in first */
+                const uint32_t b0 = (z0.b.iend - 4u) << 4, b1 = (z1.b.iend - 4u) << 4;
+                const bool r0 = want && z0.b.iend == g0, r1 = want && z1.b.iend == g1;
+                for (;;) {
+                    const bool c0 = r0 && st_crc_before(z0, b0), c1 = r1 && st_crc_before(z1, b1);
+                    if (!any_lane(c0 || c1)) break;
+                    st_crc_step(z0, c0, CT);
+                    st_crc_step(z1, c1, CT);
+                }
+            }
             wait_vm_n(nst);
             z0.b.vendw = z0.b.iend * 4u;
             z1.b.vendw = z1.b.iend * 4u;
@@ -3373,8 +3530,16 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
      * frame whose footer ends there and whose CRC was 0 is done.  Otherwise (the last frame
      * of a batch, a gap before the next offset, a mismatch) the frame is re-read here. */
     uint32_t crc = crc_read;
-    bool need = false;
     const bool defer = (ablate & BNF_MODE_DEFER_CRC) != 0; /* k_crc_join checks it */
+#if BNF_ST_RING_CRC
+    if (ok && crc_ring) { /* the in-ring CRC's last bytes (the lag behind each cursor) through global memory */
+        const uint8_t *bytes = (const uint8_t *)words;
+        const uint32_t c0 = crc16_cont_global(z0.crc, bytes, fi.frame_off + (uint32_t)(z0.ca - fo), xabs, CT);
+        const uint32_t c1 = crc16_cont_global(z1.crc, bytes, fi.frame_off + (uint32_t)(z1.ca - fo), end_byte, CT);
+        crc = crc16_shift(c0, end_byte - xabs) ^ c1;
+    }
+#else
+    bool need = false;
     if (ok && !defer) {
         const uint32_t cn = info[f].crc_next;
         const bool pre = (cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && fi.frame_off + (cn & BNF_CN_LEN) == end_byte + 2u;
@@ -3387,6 +3552,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         __syncthreads();
         if (need) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
     }
+#endif
     if (ok && crc != crc_read) ok = false;
     if (ok) {
         info[f].resume_bit = resume;
@@ -3464,13 +3630,15 @@ hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
     }
     return e;
 }
+/* seg: k_order's bucket ends (W = 16 / 32 only, with perm): blocks outside the class leave first */
 hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                     uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                                    const uint32_t *perm, uint32_t mode, hipStream_t s) {
+                                    const uint32_t *perm, uint32_t mode, const uint32_t *seg, hipStream_t s) {
     const uint32_t fpb = DEC_LANES / chn_lanes;
-    const dim3 grid((nframes + fpb - 1) / fpb);
-    hipLaunchKernelGGL((k_decode<DEC_W, 32, DEC_RD>), grid, dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes, fmt,
-                       out, out_bytes, info, perm, ablate_flags() | mode);
+    const uint32_t nb = (nframes + fpb - 1) / fpb;
+    if (DEC_W == 8 || !perm) seg = nullptr;
+    hipLaunchKernelGGL((k_decode<DEC_W, 32, DEC_RD>), dim3(nb), dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes,
+                       fmt, out, out_bytes, info, perm, ablate_flags() | mode, seg);
     return hipGetLastError();
 }
 } /* extern "C" */
@@ -3538,7 +3706,7 @@ hipError_t bnf_upload_tables_tu5(const uint8_t *, const uint16_t *, const uint16
 void bnf_set_ablate_tu5(uint32_t);
 hipError_t bnf_stats_tu5(uint64_t *, int);
 hipError_t bnf_launch_decode_tu5(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, const uint32_t *, hipStream_t);
 hipError_t bnf_upload_tables_tu1(const uint8_t *, const uint16_t *, const uint16_t *);
 hipError_t bnf_upload_tables_tu2(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu1(uint32_t);
@@ -3546,9 +3714,9 @@ void bnf_set_ablate_tu2(uint32_t);
 hipError_t bnf_stats_tu1(uint64_t *, int);
 hipError_t bnf_stats_tu2(uint64_t *, int);
 hipError_t bnf_launch_decode_tu1(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, const uint32_t *, hipStream_t);
 hipError_t bnf_launch_decode_tu2(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, const uint32_t *, hipStream_t);
 
 hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     hipError_t e = upload_tables(crc8, crc16x8, xpow);
@@ -3803,6 +3971,9 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         if (e != hipSuccess) return e;
     }
     const uint32_t mode = ev_crc ? BNF_MODE_DEFER_CRC : 0u; /* a concurrent CRC pass is running (k_crc) */
+    /* the class segments of the decode order (bucket ends), for the W16 / W32 grids */
+    static const bool seg_on = [] { const char *e = getenv("BNFLAC_DECODE_SEG"); return !e || atoi(e) != 0; }();
+    const uint32_t *seg = (perm && seg_on) ? order : nullptr;
     /* k_decode_st -> k_decode<8> on s (k_decode<8> takes k_decode_st's hand-backs);
      * k_decode<16> and k_decode<32> each on a side stream of the device, forked from s
      * before k_decode_st (default) or after it (BNFLAC_DECODE_FORK=1), and joined before
@@ -3828,9 +3999,9 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         hipError_t r = hipEventRecord(sq->fork, s);
         for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipStreamWaitEvent(sq->st[i], sq->fork, 0);
         if (r == hipSuccess)
-            r = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, sq->st[1]);
+            r = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, sq->st[1]);
         if (r == hipSuccess)
-            r = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, sq->st[0]);
+            r = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, sq->st[0]);
         for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipEventRecord(sq->join[i], sq->st[i]);
         return r;
     };
@@ -3840,7 +4011,7 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
                 ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s)
                 : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
     if (sq && fm == 1 && e == hipSuccess) e = fork();
-    if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+    if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, nullptr, s);
     if (sq) {
         for (int i = 0; i < 2; i++) { /* joined even if a launch failed */
             const hipError_t ej = hipStreamWaitEvent(s, sq->join[i], 0);
@@ -3848,8 +4019,8 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         }
         lk.unlock();
     } else {
-        if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
-        if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+        if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, s);
+        if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, s);
     }
     if (e == hipSuccess && ev_crc) {
         e = hipStreamWaitEvent(s, ev_crc, 0);

@@ -905,3 +905,76 @@ def test_reader_pool_reuse_across_sizes_and_layouts(gpu):
     finally:
         r.close()
     assert L.bnflac_reader_pool_release(0) == 1
+
+
+def _crc_cases(gpu, data, offs, base=0):
+    """Decode `data` placed at byte `base` of a device buffer; every stereo frame's CRC-16
+    (k_decode_st computes it from its two bit-reader rings, channel 0's bytes and channel 1's
+    combined by a GF(2) shift) against the CRC of the frame's bytes."""
+    import oracle
+    torch, libflac, dec = gpu
+    sp = _stream_params(libflac, data)
+    dev = torch.device("cuda:0")
+    n = base + len(data)
+    d_bytes = torch.zeros((n + 3) // 4 * 4 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[base:n] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    d_offs = torch.tensor([base + int(o) for o in offs], dtype=torch.int64, device=dev)
+    stride = libflac.out_stride(libflac.OUT_FLACDECODER, sp)
+    d_out = torch.full((sp.total_samples * stride + 64,), 0xAB, dtype=torch.uint8, device=dev)
+    d_info = torch.zeros(len(offs) * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    dec.decode_frames(d_bytes, n, d_offs, len(offs), sp, libflac.OUT_FLACDECODER, d_out, d_info)
+    torch.cuda.synchronize()
+    info = libflac.info_array(d_info.cpu().numpy())
+    del d_bytes
+    for i, o in enumerate(offs):
+        if info["status"][i] != 0:
+            continue
+        end = int(info["resume_bit"][i]) // 8 - base
+        assert info["crc16_calc"][i] == oracle.crc16(data[int(o):end - 2]), (i, o)
+        assert info["crc_ok"][i] == (oracle.crc16(data[int(o):end - 2]) == int.from_bytes(data[end - 2:end], "big"))
+    return info, d_out[: sp.total_samples * stride].cpu().numpy()
+
+
+def test_ring_crc_beyond_4gib(gpu):
+    """Frames at byte offsets past 2^32 (the rings track bytes mod 2^32): CRCs computed
+    right, PCM lossless, and a damaged frame zero-filled."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    s = synth.encode(synth.config("C2", nframes=24, seed=21))
+    data = bytearray(s.data.tobytes())
+    o = [int(x) for x in s.frame_offsets]
+    info, out = _crc_cases(gpu, bytes(data), o, base=(1 << 32) + 4099)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    assert out.tobytes() == s.pcm.astype("<i2").tobytes()
+    data[o[7] + 3000] ^= 0x10
+    info, out = _crc_cases(gpu, bytes(data), o, base=(1 << 32) - 2000)
+    assert info["crc_ok"][7] == 0 or info["status"][7] != 0
+    pcm = out.view("<i2").reshape(-1, 2)
+    assert not pcm[7 * 4096: 8 * 4096].any()
+
+
+@pytest.mark.parametrize("cfg,kw", [("C2", {}), ("C2", {"partition_order": 0, "seed": 3}),
+                                    ("C2", {"stereo_mode": 2, "seed": 4}), ("C1", {"seed": 5})])
+def test_ring_crc_damage_positions(gpu, cfg, kw):
+    """One flipped bit at 40 positions across a frame (header, channel 0, around the channel
+    split, channel 1, the footer), each its own stream: every CRC-16 the decode computes is the
+    CRC of the frame's bytes, and frames it rejects are zero-filled."""
+    from birdnest.audio_amd import synth
+    s = synth.encode(synth.config(cfg, **({"nframes": 4, "last_blocksize": 0} | kw)))
+    data = s.data.tobytes()
+    o = [int(x) for x in s.frame_offsets]
+    f = 1
+    lo, hi = o[f], o[f + 1]
+    rng = np.random.default_rng(7)
+    pos = sorted(set(np.linspace(lo, hi - 1, 40).astype(int).tolist()))
+    bad = 0
+    for p in pos:
+        d = bytearray(data)
+        d[p] ^= 1 << int(rng.integers(0, 8))
+        info, out = _crc_cases(gpu, bytes(d), o)
+        ok = info["status"][f] == 0 and info["crc_ok"][f] == 1
+        bad += not ok
+        if info["status"][f] == 0 and info["crc_ok"][f] == 0:
+            bs = int(info["blocksize"][f])
+            assert not out.view("<i2")[f * bs * 2:(f + 1) * bs * 2].any()
+    assert bad >= len(pos) - 2  # a flipped bit is (almost always) caught
