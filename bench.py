@@ -93,6 +93,8 @@ def parse_args():
     ap.add_argument("--nccl-timeout", type=int, default=180, help="seconds before a stuck collective aborts the run")
     ap.add_argument("--no-c5-flow", action="store_true",
                     help="N > 1: skip the C5 shard -> index -> decode -> RCCL gather leg")
+    ap.add_argument("--c5-batch", action="store_true",
+                    help="--config C5 as one batch of the 8 files' frames (the C5 leg's workload; --stats/--ablate apply)")
     ap.add_argument("--stats", action="store_true", help="report k_decode event counters (one extra step)")
     ap.add_argument("--ablate", default=None,
                     help="comma list of ablation bitmasks to time after the measurement (timing only, wrong output): "
@@ -585,7 +587,7 @@ def main():
     cfg = args.config
     c = CONFIGS[cfg]
 
-    if cfg == "C5":
+    if cfg == "C5" and not args.c5_batch:
         r = c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank)
         line = {"metric": METRIC}
         line.update(c5_summary(r, args, world))

@@ -1958,6 +1958,69 @@ DEV uint32_t pack_lane(const int32_t *lds, uint32_t lane, uint32_t chn_lanes, ui
     return nst;
 }
 
+/* FLACFileReader 24-bit runs (FLACFileReader.cs:220-237) flushed as wide runs: the chunk's
+ * output is fpb frame runs of CH samples x C channels x 3 bytes (CH = 32: 6C 16-byte pieces
+ * per frame); lane i writes pieces i, i + 64, ... in frame-major order, so the 64 lanes of one
+ * store cover ~1 KB of a few frames' runs instead of 64 scattered 16-byte pieces.  Each piece
+ * is 6 values (bytes 16p .. 16p+15 lie in values floor(16p/3) .. +5), read from the rows of
+ * its frame (decorrelated when stereo) and byte-aligned with v_alignbyte.  The frame table
+ * (output byte base, assignment, channels, ok) sits in the row buffer's spare columns
+ * (64..71 of rows 0..15).  Requires every frame of the wave to have a full, 16-byte-aligned
+ * chunk with C == the stream's channels (the caller checks).  Returns this lane's stores. */
+DEV uint32_t *wide_tbl(int32_t *lds, uint32_t fr) { return (uint32_t *)lds + (fr >> 1) * RP + 64u + (fr & 1u) * 4u; }
+template <int CH>
+DEV uint32_t pack_wide24(int32_t *lds, uint32_t lane, uint32_t cl, uint32_t n0, uint32_t C, uint8_t *__restrict__ out) {
+    static_assert(CH * 3 % 16 == 0 && DEC_LANES * 6 >= CH * 3 * 64 / 16, "6 pieces per lane cover a chunk");
+    const uint32_t fpb = DEC_LANES / cl, ppf = (uint32_t)CH * C * 3u / 16u, np = fpb * ppf;
+    uint32_t nst = 0;
+#pragma unroll
+    for (int u = 0; u < CH * 3 / 16; u++) {
+        const uint32_t P = (uint32_t)u * 64u + lane;
+        const uint32_t fr = P / ppf, pp = P - fr * ppf;
+        const uint32_t *t = wide_tbl(lds, min(fr, fpb - 1u));
+        const uint32_t meta = t[2];
+        if (P >= np || !((meta >> 8) & 1u)) continue;
+        const uint32_t b0 = 16u * pp, vlo = b0 / 3u, off = b0 - 3u * vlo;
+        const int32_t *rows = lds + fr * cl;
+        int32_t v[6];
+        if (C == 2u) {
+            const uint32_t q0 = vlo >> 1, odd = vlo & 1u, as = meta & 15u;
+            int32_t L[4], R[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int2 x = *(const int2 *)(rows + min(q0 + (uint32_t)q, (uint32_t)CH - 1u) * RP);
+                L[q] = x.x;
+                R[q] = x.y;
+                decorrelate(as, L[q], R[q]);
+            }
+            v[0] = odd ? R[0] : L[0];
+            v[1] = odd ? L[1] : R[0];
+            v[2] = odd ? R[1] : L[1];
+            v[3] = odd ? L[2] : R[1];
+            v[4] = odd ? R[2] : L[2];
+            v[5] = odd ? L[3] : R[2];
+        } else {
+            uint32_t q = vlo / C, c = vlo - q * C;
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                v[i] = rows[q * RP + c];
+                if (++c == C) { c = 0; q++; }
+            }
+        }
+        const uint32_t d0 = ((uint32_t)v[0] & 0xFFFFFFu) | ((uint32_t)v[1] << 24);
+        const uint32_t d1 = (((uint32_t)v[1] >> 8) & 0xFFFFu) | ((uint32_t)v[2] << 16);
+        const uint32_t d2 = (((uint32_t)v[2] >> 16) & 0xFFu) | ((uint32_t)v[3] << 8);
+        const uint32_t d3 = ((uint32_t)v[4] & 0xFFFFFFu) | ((uint32_t)v[5] << 24);
+        const uint32_t d4 = ((uint32_t)v[5] >> 8) & 0xFFFFu;
+        const uint64_t ob = (((uint64_t)t[1] << 32) | t[0]) + (uint64_t)n0 * C * 3u + b0;
+        gst128((uint64_t)(uintptr_t)out + ob,
+               u32x4{__builtin_amdgcn_alignbyte(d1, d0, off), __builtin_amdgcn_alignbyte(d2, d1, off),
+                     __builtin_amdgcn_alignbyte(d3, d2, off), __builtin_amdgcn_alignbyte(d4, d3, off)});
+        nst++;
+    }
+    return nst;
+}
+
 /* restore-path dispatch (per lane); the tap count is the instance's (orders below it run
  * with zero coefficients), so a wave takes at most one variant per libFLAC path */
 #define LPC_DISPATCH(FN, ...)                                                                     \
@@ -2076,6 +2139,14 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
     const uint32_t fbs = fok ? f_bs[fl] : 0u, fch = have ? fi.channels : 0u, fas = fok ? f_as[fl] : 0u;
     const uint64_t fos = fok ? f_out[fl] : 0u;
     lds_sync(); /* the ring's first DMA may overwrite the tables only after these reads */
+    const bool wide_fmt = fmt == BNF_OUT_FILEREADER && sp.bps == 24u && !(ablate & 0x2000u);
+    if (wide_fmt && fl < fpb && ch == 0) { /* pack_wide24's frame table (row buffer spare columns) */
+        uint32_t *t = wide_tbl(lds, fl);
+        const uint64_t ob = fos * sp.channels * 3u;
+        t[0] = (uint32_t)ob;
+        t[1] = (uint32_t)(ob >> 32);
+        t[2] = fas | (fch << 4) | ((fok ? 1u : 0u) << 8);
+    }
     const uint64_t f_off = have ? fi.frame_off : 0u;
 
     /* ---- subframe setup */
@@ -2219,10 +2290,19 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
         case BNF_OUT_FLACDECODER:
             pk = pack_lane<BNF_OUT_FLACDECODER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels, 0, out);
             break;
-        default:
-            pk = pack_lane<BNF_OUT_FILEREADER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels,
-                                                    sp.bps == 24 ? 3u : 2u, out);
+        default: {
+            bool wide = false;
+            if (CHK == 32 && wide_fmt) { /* every frame of the wave: a full aligned chunk of all the stream's channels */
+                const bool bad = have && fok && !(fch == sp.channels && n0 + CHK <= fbs &&
+                                                  (((fos + n0) * sp.channels * 3u) & 15u) == 0u);
+                wide = !any_lane(bad);
+            }
+            if (wide) pk = pack_wide24<CHK>(lds, lane, chn_lanes, n0, sp.channels, out);
+            else
+                pk = pack_lane<BNF_OUT_FILEREADER, CHK>(lds, lane, chn_lanes, n0, fok, fbs, fch, fas, fos, sp.channels,
+                                                        sp.bps == 24 ? 3u : 2u, out);
             break;
+        }
         }
         /* account this chunk's stores for the next refill's counted vmcnt wait: every store
          * of a lane is a store instruction of the wave, so the wave issued at least the

@@ -131,7 +131,8 @@ static int ensure_device(int dev) {
 
 /* Timing experiments only (bench.py --ablate): skip parts of the kernels.  Results are
  * wrong while non-zero.  bit0 CRC-16, bit1 PCM stores, bit2 restore, bit3 Rice decode,
- * bit4 k_parse subframe walk. */
+ * bit4 k_parse subframe walk.  0x2000 is an exact A/B switch: the 24-bit FLACFileReader
+ * wide flush (pack_wide24) off. */
 extern "C" BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags) { bnf_set_ablate(flags); }
 /* Coalesced CRC pass of the batch API (frame record crc_next; the decode kernels then skip
  * their own CRC re-read for frames it vouches for).  1: fused into the k_parse launch;
