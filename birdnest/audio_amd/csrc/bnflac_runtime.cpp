@@ -152,6 +152,10 @@ extern "C" BNFLAC_API void bnflac_debug_set_crc_pass(int on) { g_crc_pass = std:
 extern "C" void bnf_set_parse_wave(int mode);
 /* parse kernel: -1 auto (k_parse_wave for small launches), 0 k_parse, 1 k_parse_wave (tests, A/B) */
 extern "C" BNFLAC_API void bnflac_debug_set_parse_wave(int mode) { bnf_set_parse_wave(mode); }
+extern "C" void bnf_set_decode_wave(int mode);
+/* decode kernels: -1 auto (k_decode_wave for small launches), 0 the lane kernels, 1 k_decode_wave
+ * whenever the rows fit (tests, A/B) */
+extern "C" BNFLAC_API void bnflac_debug_set_decode_wave(int mode) { bnf_set_decode_wave(mode); }
 extern "C" hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset);
 /* k_parse_wave's debug counters (collected when BNFLAC_PW_STATS is set): passes, splice rounds,
  * serial fallbacks, partitions, frames, wave-cycles in scans.  out8: 8 values. */

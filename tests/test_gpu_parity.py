@@ -36,6 +36,20 @@ def gpu():
     return torch, libflac, libflac.BatchDecoder(0)
 
 
+@pytest.fixture
+def decode_mode(request, gpu):
+    """bnflac_debug_set_decode_wave for one test: 0 the lane kernels (k_decode_st / k_decode<W>),
+    1 the wave-per-frame k_decode_wave, -1 auto (small batches take the wave kernel)."""
+    torch, libflac, _ = gpu
+    L = libflac.load()
+    L.bnflac_debug_set_decode_wave(request.param)
+    yield request.param
+    L.bnflac_debug_set_decode_wave(-1)
+
+
+LANE = pytest.mark.parametrize("decode_mode", [0], indirect=True)  # tests of the lane kernels' own paths
+
+
 def _stream_params(libflac, data: bytes):
     """STREAMINFO -> StreamParams (host parse of the 34-byte block, like MetadataCallback)."""
     si = data[8:42]
@@ -103,8 +117,9 @@ def test_rfc9639_example2_frame1_gpu(gpu):
     assert _sha(pcm) == g["pcm_sha256_oracle"]
 
 
+@pytest.mark.parametrize("decode_mode", [0, 1], indirect=True)
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
-def test_config_batch_vs_oracle_and_source(gpu, cfg):
+def test_config_batch_vs_oracle_and_source(gpu, cfg, decode_mode):
     import oracle
     from birdnest.audio_amd import synth
     torch, libflac, _ = gpu
@@ -121,7 +136,8 @@ def test_config_batch_vs_oracle_and_source(gpu, cfg):
 
 @pytest.mark.parametrize("order,prec,stereo", [(2, 15, 0), (3, 0, 3), (4, 12, 0), (8, 15, 1), (8, 0, 2),
                                                 (12, 15, 3), (16, 0, 0), (32, 15, 3), (32, 0, 0)])
-def test_lpc_restore_paths_16bit(gpu, order, prec, stereo):
+@pytest.mark.parametrize("decode_mode", [0, 1], indirect=True)
+def test_lpc_restore_paths_16bit(gpu, order, prec, stereo, decode_mode):
     """Every libFLAC restore path on 16-bit input (MMX for order >= 4 at <= 32 bits, ia32
     for low orders, the 64-bit path when bps + precision + log2(order) > 32 -- no encoder
     precision clamp here), in both k_decode instances (orders <= 8 and above)."""
@@ -518,7 +534,8 @@ FL_ST, FL_REDO = 32, 64
 @pytest.mark.parametrize("cfg,kw", [("C1", {}), ("C2", {}), ("C2", {"stereo_mode": 1}), ("C2", {"stereo_mode": 2}),
                                     ("C2", {"stereo_mode": 3}), ("C2", {"partition_order": 0}),
                                     ("C2", {"blocksize": 1152}), ("C1", {"blocksize": 4000})])
-def test_stereo_fast_path_layouts(gpu, fmt_name, cfg, kw):
+@LANE
+def test_stereo_fast_path_layouts(gpu, fmt_name, cfg, kw, decode_mode):
     """k_decode_st (one lane per stereo frame) writes every layout bit-exactly, and takes
     the frames itself (BNF_FL_ST set, no hand-back) on regular streams -- including a
     blocksize that is not a multiple of its 32-sample chunk (general path for the tail)."""
@@ -551,7 +568,8 @@ def test_stereo_fast_path_layouts(gpu, fmt_name, cfg, kw):
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C4"])
-def test_stereo_handback_matches(gpu, cfg):
+@LANE
+def test_stereo_handback_matches(gpu, cfg, decode_mode):
     """With k_decode_st disabled (ablation 0x400) every stereo frame goes to k_decode<8>;
     both routes give identical PCM and frame records."""
     from birdnest.audio_amd import synth
@@ -571,7 +589,8 @@ def test_stereo_handback_matches(gpu, cfg):
 
 
 @pytest.mark.parametrize("stereo_mode", [1, 2, 3])
-def test_stereo_side_beyond_int16_handed_back(gpu, stereo_mode):
+@LANE
+def test_stereo_side_beyond_int16_handed_back(gpu, stereo_mode, decode_mode):
     """k_decode_st's dot2 predictor is exact only while samples fit int16.  Loud,
     weakly correlated channels push the 17-bit side channel past that: those frames must be
     handed back (BNF_FL_REDO) and come out of k_decode<8> bit-exact."""
