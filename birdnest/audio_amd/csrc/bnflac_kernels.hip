@@ -949,18 +949,19 @@ DEV bool wave_rice_skip(WR &r, uint32_t cnt, uint32_t k, uint64_t limit, bool st
         const uint64_t tw0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
         wr_need(r, ws, ws + 64u * SW + (DEC ? 1u : 0u)); /* DEC: a last codeword's low bits may reach one word further */
         if (stats) pw_stat(r, true, 6, __builtin_amdgcn_s_memtime() - tw0);
-        uint32_t w[SW + 1];
+        uint32_t w[SW + 2]; /* w[SW + 1]: only DEC reads it (a last codeword's low bits) */
 #pragma unroll
-        for (int j = 0; j <= SW; j++) w[j] = wr_word(r, ws + SW * lane + (uint32_t)j);
+        for (int j = 0; j <= SW + (DEC ? 1 : 0); j++) w[j] = wr_word(r, ws + SW * lane + (uint32_t)j);
         /* 1. speculative walk of this lane's segment from its first bit (lane 0: the cursor).
          * `slow` only matters if the lane turns out to lie inside the partition. */
         uint32_t ent = lane ? 0u : e0;
-        uint32_t m[SW], none[SW];
-#pragma unroll
-        for (int j = 0; j < SW; j++) none[j] = 0u;
+        uint32_t m[SW];
         bool slow, merged;
         const uint32_t nsteps = 31u / k1 + 1u; /* codeword starts per word, at most */
-        uint32_t exit = seg_walk<SW, false>(w, ent, k1, nsteps, none, m, slow, merged);
+        uint32_t none[SW];
+#pragma unroll
+        for (int j = 0; j < SW; j++) none[j] = 0u;
+        uint32_t exit = seg_walk<SW, false>((const uint32_t(&)[SW + 1])w, ent, k1, nsteps, none, m, slow, merged);
         if (slow) exit = SB;
         /* 2. splice: a lane whose true entry (the previous lane's exit - SB) differs re-walks
          * from it until it meets a start of its own walk (the paths coincide from there) or
@@ -981,7 +982,7 @@ DEV bool wave_rice_skip(WR &r, uint32_t cnt, uint32_t k, uint64_t limit, bool st
                 } else {
                     uint32_t nm[SW];
                     bool s2, mg;
-                    const uint32_t pos = seg_walk<SW, true>(w, te, k1, nsteps, m, nm, s2, mg);
+                    const uint32_t pos = seg_walk<SW, true>((const uint32_t(&)[SW + 1])w, te, k1, nsteps, m, nm, s2, mg);
                     if (mg) { /* merged at pos: the old starts from pos on, its exit and slow flag hold */
 #pragma unroll
                         for (int j = 0; j < SW; j++) {
@@ -1020,18 +1021,19 @@ DEV bool wave_rice_skip(WR &r, uint32_t cnt, uint32_t k, uint64_t limit, bool st
                 after[j] = nf;
                 if (m[j]) nf = 32u * (uint32_t)j + (uint32_t)__builtin_ctz(m[j]);
             }
-            const uint32_t segw = ws + SW * lane;
             uint32_t i = incl - n;
 #pragma unroll
             for (int j = 0; j < SW; j++) {
+                /* a codeword starting in word j ends (its k low bits) within words j .. j + 2 */
+                const uint64_t p01 = ((uint64_t)w[j] << 32) | w[j + 1], p12 = ((uint64_t)w[j + 1] << 32) | w[j + 2];
                 uint32_t mm = m[j];
                 while (mm && i < cnt) {
-                    const uint32_t pos = 32u * (uint32_t)j + (uint32_t)__builtin_ctz(mm);
+                    const uint32_t pos = (uint32_t)__builtin_ctz(mm);
                     mm &= mm - 1u;
-                    const uint32_t next = mm ? 32u * (uint32_t)j + (uint32_t)__builtin_ctz(mm) : after[j];
+                    const uint32_t next = mm ? (uint32_t)__builtin_ctz(mm) : after[j] - 32u * (uint32_t)j; /* from word j */
                     const uint32_t q = next - pos - k1, g = next - k; /* the k low bits end at the next start */
-                    const uint32_t wa = wr_word(r, segw + (g >> 5)), wb = wr_word(r, segw + (g >> 5) + 1u);
-                    const uint32_t bits = (g & 31u) ? __builtin_amdgcn_alignbit(wa, wb, 32u - (g & 31u)) : wa;
+                    const uint64_t pp = g >= 32u ? p12 : p01;
+                    const uint32_t bits = (uint32_t)((pp << (g & 31u)) >> 32);
                     const uint32_t lsb = k ? bits >> (32u - k) : 0u;
                     dst[i] = rice_zigzag((q << k) | lsb);
                     i++;
@@ -3865,40 +3867,55 @@ struct DwHdr { /* a channel's restore parameters (LDS table) */
     uint32_t type, order, wasted, path;
     int32_t shift, cval;
 };
-/* pred_at with the taps oldest first: the newest sample enters each MAC chain last, so in the
- * unrolled, branch-free restore the older taps' MACs issue while the previous sample is still
- * being computed and one MAC per chain stays on the sample-to-sample path */
-template <int T, int W>
+/* The restore of one channel on one lane (k_decode's exact predictor, pred_at).  The taps
+ * oldest first in four MAC chains and the newest tap last (the older taps' MACs issue while the
+ * previous sample is still being computed), the chains kept apart by an opaque non-volatile
+ * asm (the compiler would re-associate them into one chain; a volatile one also pinned the LDS
+ * loads behind it).  N24: libFLAC's 32-bit paths (ia32, MMX16, FIXED, CONSTANT) want the low 32
+ * bits of the sum, which v_mad_i32_i24 gives exactly while every history value fits 24 bits
+ * (coefficients always do: qlp precision <= 15); a group of W samples that leaves that range
+ * is restored again with the 64-bit MACs, which the channel keeps from then on. */
+template <int T, int W, bool N24>
 DEV int32_t dw_pred(const int32_t (&c)[W], const int32_t (&x)[W], const int32_t (&xt)[4], const Pred &p) {
-    int64_t s0 = 0, s1 = 0;
+    if constexpr (N24) {
+        int32_t a[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int u = 0; u < W; u++) {
-#ifdef DW_FWD /* A/B: newest tap first */
-        const int t = u;
-#else
-        const int t = W - 1 - u;
-#endif
-        const int32_t hv = (t < 4) ? xt[(T - 1 - t) & 3] : x[((T - 1 - t) % W + W) % W];
-        if (t & 1) s1 += (int64_t)c[t] * (int64_t)hv;
-        else s0 += (int64_t)c[t] * (int64_t)hv;
+        for (int u = 0; u < W - 1; u++) {
+            const int t = W - 1 - u;
+            const int32_t hv = (t < 4) ? xt[(T - 1 - t) & 3] : x[((T - 1 - t) % W + W) % W];
+            a[t & 3] = (int32_t)((uint32_t)a[t & 3] + (uint32_t)__mul24(c[t], hv));
+        }
+        asm("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
+        const uint32_t S = ((uint32_t)a[0] + (uint32_t)a[1]) + ((uint32_t)a[2] + (uint32_t)a[3]) +
+                           (uint32_t)__mul24(c[0], xt[(T - 1) & 3]);
+        return (int32_t)S >> p.sh;
+    } else {
+        int64_t a[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < W - 1; u++) { /* taps W-1 .. 1: samples older than the newest */
+            const int t = W - 1 - u;
+            const int32_t hv = (t < 4) ? xt[(T - 1 - t) & 3] : x[((T - 1 - t) % W + W) % W];
+            a[t & 3] += (int64_t)c[t] * (int64_t)hv;
+        }
+        asm("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
+        const int64_t S = ((a[0] + a[1]) + (a[2] + a[3])) + (int64_t)c[0] * (int64_t)xt[(T - 1) & 3]; /* newest last */
+        return p.wide ? (int32_t)(S >> p.sh) : ((int32_t)S >> p.sh);
     }
-    asm volatile("" : "+v"(s0), "+v"(s1));
-    const int64_t S = s0 + s1;
-    return p.wide ? (int32_t)(S >> p.sh) : ((int32_t)S >> p.sh);
 }
-template <int T, int W>
-DEV void dw_restore_steps(int32_t *buf, const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4], const Pred &p,
-                          uint32_t j, uint32_t bs) {
+template <int T, int W, bool N24>
+DEV void dw_restore_steps(int32_t *buf, const int32_t (&v)[W], const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4],
+                          const Pred &p, uint32_t j, uint32_t &oor) {
     if constexpr (T < W) {
-        const int32_t v = buf[j + T];
-        const int32_t pr = dw_pred<T, W>(c, x, xt, p);
-        const int32_t s = (j + (uint32_t)T < p.order) ? v : (int32_t)((uint32_t)v + (uint32_t)pr);
+        const int32_t pr = dw_pred<T, W, N24>(c, x, xt, p);
+        const int32_t s = (j + (uint32_t)T < p.order) ? v[T] : (int32_t)((uint32_t)v[T] + (uint32_t)pr);
+        if (N24) oor |= ((uint32_t)s + 0x800000u) >> 24; /* s outside [-2^23, 2^23) */
         push_at<T, W>(x, xt, p, s);
-        if (j + (uint32_t)T < bs) buf[j + T] = (int32_t)((uint32_t)s << p.wasted);
-        dw_restore_steps<T + 1, W>(buf, c, x, xt, p, j, bs);
+        buf[j + T] = (int32_t)((uint32_t)s << p.wasted); /* rows past bs are padding: no branch between samples */
+        dw_restore_steps<T + 1, W, N24>(buf, v, c, x, xt, p, j, oor);
     }
 }
-/* lane ch < C restores its channel's rows in place (residuals / warm-ups in, samples out) */
+/* lane ch < C restores its channel's rows in place (residuals / warm-ups in, samples out);
+ * called by those lanes only (the range test is a ballot over them) */
 template <int W>
 DEV void dw_restore(int32_t *buf, uint32_t bs, const int32_t *ctab, const DwHdr &h) {
     int32_t c[W], x[W], xt[4];
@@ -3930,8 +3947,29 @@ DEV void dw_restore(int32_t *buf, uint32_t bs, const int32_t *ctab, const DwHdr 
         c[0] = 1;
         pd.order = 1;
     }
+    bool n24 = !any_lane(pd.wide); /* the 64-bit path needs the exact sum */
 #pragma unroll 1
-    for (uint32_t j = 0; j < bs; j += W) dw_restore_steps<0, W>(buf, c, x, xt, pd, j, bs);
+    for (uint32_t j = 0; j < bs; j += W) {
+        int32_t v[W];
+#pragma unroll
+        for (int t = 0; t < W; t++) v[t] = buf[j + t];
+        uint32_t oor = 0;
+        if (n24) {
+            int32_t x0[W], xt0[4];
+#pragma unroll
+            for (int t = 0; t < W; t++) x0[t] = x[t];
+#pragma unroll
+            for (int t = 0; t < 4; t++) xt0[t] = xt[t];
+            dw_restore_steps<0, W, true>(buf, v, c, x, xt, pd, j, oor);
+            if (!any_lane(oor != 0u)) continue;
+            n24 = false; /* a value left 24 bits: this group again, exactly, and the rest too */
+#pragma unroll
+            for (int t = 0; t < W; t++) x[t] = x0[t];
+#pragma unroll
+            for (int t = 0; t < 4; t++) xt[t] = xt0[t];
+        }
+        dw_restore_steps<0, W, false>(buf, v, c, x, xt, pd, j, oor);
+    }
 }
 
 __global__ void __launch_bounds__(64) k_decode_wave(const uint32_t *__restrict__ words, uint64_t nbytes, uint32_t nframes,

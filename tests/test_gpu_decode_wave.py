@@ -150,3 +150,18 @@ def test_frames_wider_than_streaminfo_handed_back(gpu):
     assert n == 50
     info, _, _ = _decode(gpu, data, _offsets(s), libflac.OUT_FLACDECODER, 1, _sp(libflac, data, 1024))
     assert (info["flags"] & 512).any() and not (info["flags"][info["blocksize"] <= 1024] & 512).any()
+
+
+@pytest.mark.parametrize("order,stereo", [(2, 3), (4, 1), (3, 0)])
+def test_fixed_24bit_side_leaves_24_bits(gpu, order, stereo):
+    """FIXED subframes of 24-bit stereo (the side channel has 25 bits): the wave restore's
+    24-bit MACs see history values past 24 bits, restore those groups again with 64-bit MACs,
+    and stay identical to the lane kernels."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _, _ = gpu
+    s = synth.encode(synth.config("C3", nframes=6, last_blocksize=0, subframe_mode=synth.SUB_FIXED, order=order,
+                                  stereo_mode=stereo, level=0.95, noise=0.3, wasted_bits_max=0, seed=40 + order))
+    data = s.data.tobytes()
+    assert _same(gpu, data, _offsets(s), libflac.OUT_INTERLEAVED32) == 6
+    info, out, _ = _decode(gpu, data, _offsets(s), libflac.OUT_INTERLEAVED32, 1, _sp(libflac, data))
+    assert np.array_equal(out[:s.nsamples * 8].view("<i4").reshape(-1, 2), s.pcm)
