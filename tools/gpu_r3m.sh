@@ -5,13 +5,13 @@ tail -2 gpurun_out/r3m_tests.log
 run() { # name lib env...
   local v=$1 lib=$2; shift 2
   cp ab/$lib.so birdnest/audio_amd/lib/libbnflac.so
-  env "$@" timeout -k 10 300 python bench.py --config C3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-index --no-reader --legs=C5 --out gpurun_out/r3m_${v}.json > /dev/null 2>&1 || { echo fail $v; exit 1; }
+  env "$@" timeout -k 10 300 python bench.py --config C3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --no-index --no-reader --legs=C5,C4 --out gpurun_out/r3m_${v}.json > /dev/null 2>&1 || { echo fail $v; exit 1; }
   python3 -c "
 import json; d=json.load(open('gpurun_out/r3m_${v}.json'))
 print('$v', 'C3', d['roofline']['avg_launch_ms'], d['bitexact'], [(k, v['roofline']['avg_launch_ms'], v['bitexact']) for k,v in d['legs'].items()])"
 }
 for r in 1 2; do
 run base$r base X=1
-run wide$r wide X=1
+run pre$r pre X=1
 done
-cp ab/wide.so birdnest/audio_amd/lib/libbnflac.so
+cp ab/pre.so birdnest/audio_amd/lib/libbnflac.so
