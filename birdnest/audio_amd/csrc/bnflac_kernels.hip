@@ -33,6 +33,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <mutex>
+#include <type_traits>
 
 #include "bnflac_device.h"
 
@@ -105,6 +106,10 @@ DEV void gst128(uint64_t addr, u32x4 v) { *(__attribute__((address_space(1))) u3
 #define BNF_MODE_DEFER_CRC 0x1000u
 /* Mode bit: the lane kernels decode only the frames k_decode_wave handed back (BNF_FL_WAVE_REDO). */
 #define BNF_MODE_WREDO 0x4000u
+/* Mode bit: k_decode_sw ran before the other lane kernels (they take its SW frames only when
+ * it handed them back).  Host ablation bit BNF_ABLATE_NO_SW: do not launch it. */
+#define BNF_MODE_SW 0x8000u
+#define BNF_ABLATE_NO_SW 0x10000u
 
 /* ----------------------------------------------------------------- bit reader */
 #define RING_MAX 16       /* 16-byte slots per lane (k_parse and k_decode_st use 8) */
@@ -1307,6 +1312,7 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
         if (maxorder > 16) fi.flags |= BNF_FL_W32;
         else if (maxorder > 8 || (maxorder > 0 && fi.bps > 16)) fi.flags |= BNF_FL_W16;
         else if (fi.channels == 2 && fi.bps <= 16 && !raw) fi.flags |= BNF_FL_ST;
+        if (maxorder > 0 && maxorder <= 12 && fi.channels == 2 && fi.bps > 16 && fi.bps <= 24 && !raw) fi.flags |= BNF_FL_SW;
     }
     fi.status = st;
 #pragma unroll
@@ -1775,6 +1781,7 @@ __global__ void __launch_bounds__(64) k_parse_wave(const uint32_t *__restrict__ 
         if (maxorder > 16) fi.flags |= BNF_FL_W32;
         else if (maxorder > 8 || (maxorder > 0 && fi.bps > 16)) fi.flags |= BNF_FL_W16;
         else if (fi.channels == 2 && fi.bps <= 16 && !raw) fi.flags |= BNF_FL_ST;
+        if (maxorder > 0 && maxorder <= 12 && fi.channels == 2 && fi.bps > 16 && fi.bps <= 24 && !raw) fi.flags |= BNF_FL_SW;
     }
     fi.status = st;
 #pragma unroll
@@ -2135,9 +2142,12 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
     bnf_frame_info fi;
     bool have = (fl < fpb) && (f < nframes);
     if (ablate & BNF_MODE_WREDO) have = have && (info[f].flags & BNF_FL_WAVE_REDO); /* after k_decode_wave: its hand-backs */
+    /* k_decode_sw's frames (BNF_MODE_SW: it ran first) are this kernel's only once handed back */
+    const bool sw_on = (ablate & BNF_MODE_SW) != 0;
     if (MAXW != 8) { /* most blocks are not this instance's: leave on two words of the record */
-        const bool w = have && info[f].status == BNF_ST_OK && (info[f].flags & (BNF_FL_W16 | BNF_FL_W32)) &&
-                       !(info[f].flags & BNF_FL_ST);
+        const uint32_t fl = have ? info[f].flags : 0u;
+        const bool w = have && info[f].status == BNF_ST_OK && (fl & (BNF_FL_W16 | BNF_FL_W32)) && !(fl & BNF_FL_ST) &&
+                       !(sw_on && (fl & BNF_FL_SW) && !(fl & BNF_FL_REDO));
         if (!__any(w)) return;
     } else { /* W = 8: narrow non-stereo frames, and stereo frames k_decode_st handed back */
         bool w = false;
@@ -2154,6 +2164,7 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
      * ST frames (the ST bit is k_parse's and does not change; REDO may be being set). */
     const bool st_frame = have && (fi.flags & BNF_FL_ST) && !(ablate & 0x400u);
     if (st_frame && (MAXW != 8 || !(fi.flags & BNF_FL_REDO))) have = false;
+    if (have && sw_on && (fi.flags & BNF_FL_SW) && !(fi.flags & BNF_FL_REDO)) have = false;
     bool frame_ok = have && fi.status == BNF_ST_OK;
     /* one wave per workgroup: the W = 8, 16 and 32 instances split the blocks between them
      * by the widest class among the block's non-ST frames (k_parse's flags); the W = 8
@@ -2746,7 +2757,7 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
 }
 #endif /* BNF_TU == 0 */
 
-#if BNF_TU == 3 || BNF_TU == 4
+#if BNF_TU == 3 || BNF_TU == 4 || BNF_TU == 7 /* TU 7: k_decode_sw, on the same helpers */
 /* =============================================================== k_decode_st
  * Stereo fast path: one lane per 2-channel frame (both subframes, two independent bit
  * cursors), 64 frames per single-wave workgroup.  Same arithmetic as k_decode (read_frame_
@@ -2795,6 +2806,13 @@ DEV uint32_t st_pk(int32_t lo, int32_t hi) { return __builtin_amdgcn_perm((uint3
 typedef short st_s2 __attribute__((ext_vector_type(2)));
 DEV int32_t st_d2(uint32_t a, uint32_t b, int32_t acc) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(st_s2, a), __builtin_bit_cast(st_s2, b), acc, false);
+}
+/* dot2 with a zero accumulator: the VOP3P form takes the inline 0 (the compiler picks
+ * v_dot2c, whose accumulator is its destination, and copies a zero register into it first) */
+DEV int32_t st_d2z(uint32_t a, uint32_t b) {
+    int32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
 /* subframe header -> fast-path state; false: hand the frame back */
@@ -2852,7 +2870,8 @@ DEV bool st_setup(StCh &z, uint32_t bps, uint32_t bs, uint64_t limit) {
     return true;
 }
 
-DEV void st_partition(StCh &z) { /* read_residual_partitioned_rice_ @0x10012da0 */
+template <class Z>
+DEV void st_partition(Z &z) { /* read_residual_partitioned_rice_ @0x10012da0 */
     const uint32_t kk = br_read(z.b, z.plen);
     z.left = (z.porder == 0 || z.pidx > 0) ? z.psamples : z.psamples - z.order;
     if (kk < z.pesc) {
@@ -2895,7 +2914,8 @@ DEV void st_adv(BR &b, uint32_t n, uint32_t nst) {
 }
 
 /* one Rice codeword of a non-escaped partition (@0x10001b30 semantics, zig-zag) */
-DEV int32_t st_rice(StCh &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
+template <class Z>
+DEV int32_t st_rice(Z &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
     const uint32_t w = br_peek(z.b);
     const uint32_t q = ffbh(w); /* ~0u for an empty window: slow */
     const bool slow = q >= z.k32; /* prefix + stop bit + k bits overrun the 32-bit window */
@@ -2914,7 +2934,8 @@ DEV int32_t st_rice(StCh &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
 }
 
 /* next residual, any partition state (warm-up excluded) */
-DEV int32_t st_next(StCh &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
+template <class Z>
+DEV int32_t st_next(Z &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
     while (z.left == 0) {
         if (z.pidx >= z.nparts) {
             trunc = 1;
@@ -2932,8 +2953,8 @@ DEV int32_t st_next(StCh &z, uint64_t limit, uint32_t &trunc, uint32_t nst) {
 template <int I>
 DEV void st_dot2(const StCh &a, const StCh &b, int32_t &pa, int32_t &pb) {
 #define Q_(z, j) z.q[(I + 8 - (j)) & 7]
-    pa = st_d2(a.cp[3], Q_(a, 7), st_d2(a.cp[2], Q_(a, 5), st_d2(a.cp[1], Q_(a, 3), st_d2(a.cp[0], Q_(a, 1), 0))));
-    pb = st_d2(b.cp[3], Q_(b, 7), st_d2(b.cp[2], Q_(b, 5), st_d2(b.cp[1], Q_(b, 3), st_d2(b.cp[0], Q_(b, 1), 0))));
+    pa = st_d2(a.cp[3], Q_(a, 7), st_d2(a.cp[2], Q_(a, 5), st_d2(a.cp[1], Q_(a, 3), st_d2z(a.cp[0], Q_(a, 1)))));
+    pb = st_d2(b.cp[3], Q_(b, 7), st_d2(b.cp[2], Q_(b, 5), st_d2(b.cp[1], Q_(b, 3), st_d2z(b.cp[0], Q_(b, 1)))));
 #undef Q_
 }
 
@@ -2943,8 +2964,8 @@ DEV void st_dot2(const StCh &a, const StCh &b, int32_t &pa, int32_t &pb) {
 template <int T>
 DEV void st_pre2(const StCh &a, const StCh &b, int32_t &pa, int32_t &pb) {
 #define P_(z, j) z.q[(T + 8 - (j)) & 7]
-    pa = st_d2(a.cp[3], P_(a, 6), st_d2(a.cp[2], P_(a, 4), st_d2(a.cp[1], P_(a, 2), 0)));
-    pb = st_d2(b.cp[3], P_(b, 6), st_d2(b.cp[2], P_(b, 4), st_d2(b.cp[1], P_(b, 2), 0)));
+    pa = st_d2(a.cp[3], P_(a, 6), st_d2(a.cp[2], P_(a, 4), st_d2z(a.cp[1], P_(a, 2))));
+    pb = st_d2(b.cp[3], P_(b, 6), st_d2(b.cp[2], P_(b, 4), st_d2z(b.cp[1], P_(b, 2))));
 #undef P_
 }
 /* pred = dot2(cp[0], q[n-1]) + pre for both channels (the critical-path pair) */
@@ -2974,6 +2995,31 @@ DEV void st_decor4(bool uni, uint32_t as_u, uint32_t as, int32_t (&L)[4], int32_
             const uint32_t side = (uint32_t)R[q], mid = ((uint32_t)L[q] << 1) | (side & 1u);
             L[q] = (int32_t)(mid + side) >> 1;
             R[q] = (int32_t)(mid - side) >> 1;
+        }
+    }
+}
+
+/* The same with the wave's assignment known at compile time (AS >= 0; AS < 0: st_decor4).
+ * Only for waves without wasted bits: the samples are then int16 (k_decode_st hands back a
+ * frame that leaves int16), so M/S needs no 32-bit wrap and takes its 4-instruction form,
+ * L = M + ((S + 1) >> 1), R = L - S: (2M + (S & 1) + S) >> 1 = M + ((S + (S & 1)) >> 1), and
+ * S + (S & 1) and S + 1 halve to the same floor for both parities of S. */
+template <int AS>
+DEV void st_decor4t(bool uni, uint32_t as_u, uint32_t as, int32_t (&L)[4], int32_t (&R)[4]) {
+    if (AS < 0) {
+        st_decor4(uni, as_u, as, L, R);
+    } else if (AS == 1) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) R[q] = L[q] - R[q];
+    } else if (AS == 2) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) L[q] = L[q] + R[q];
+    } else if (AS == 3) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int32_t l = L[q] + ((R[q] + 1) >> 1);
+            R[q] = l - R[q];
+            L[q] = l;
         }
     }
 }
@@ -3177,7 +3223,8 @@ DEV void st_resync(BR &b, uint32_t lane) { /* after generic-reader moves: ra, vl
 /* rare cases of a fused step, per channel: the cursor entered ring words not known to have
  * landed (wait for the DMAs, read the word again), or a unary prefix too long for the window
  * (the lane did not advance: decode the codeword with the generic reader) */
-DEV void st_rare(StCh &z, bool sl, bool ld, uint32_t &u, uint64_t limit, uint32_t &trunc, uint32_t nst,
+template <class Z>
+DEV void st_rare(Z &z, bool sl, bool ld, uint32_t &u, uint64_t limit, uint32_t &trunc, uint32_t nst,
                 uint32_t lane) {
     if (any_lane(ld)) {
         st_land(z.b, nst); /* lands the next two words (the check runs every other step) */
@@ -3302,7 +3349,7 @@ DEV void st_fused_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
 
 /* The restore and output half of st_fused_step for sample T of both channels, given the
  * folded Rice values u0 / u1 (zig-zag applied here). */
-template <int T, int FMT>
+template <int T, int FMT, int AS = -1>
 DEV void st_lpc_out(StCh &z0, StCh &z1, uint32_t u0, uint32_t u1, int32_t (&L)[4], int32_t (&R)[4], bool as_uni,
                     uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al, uint32_t bs, bool store,
                     u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1, bool anyw) {
@@ -3323,14 +3370,14 @@ DEV void st_lpc_out(StCh &z0, StCh &z1, uint32_t u0, uint32_t u1, int32_t (&L)[4
     L[T & 3] = s0;
     R[T & 3] = s1;
     if ((T & 3) == 3) {
-        if (__builtin_expect(anyw, 0)) { /* wasted bits (wave-uniform test) */
+        if (AS < 0 && __builtin_expect(anyw, 0)) { /* wasted bits (wave-uniform test; AS >= 0: none) */
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 L[q] = (int32_t)((uint32_t)L[q] << z0.wasted);
                 R[q] = (int32_t)((uint32_t)R[q] << z1.wasted);
             }
         }
-        st_decor4(as_uni, as_u, as, L, R);
+        st_decor4t<AS>(as_uni, as_u, as, L, R);
         if (STG) {
             uint32_t w[4];
 #pragma unroll
@@ -3388,7 +3435,7 @@ DEV void st_rare_pair(StCh &z, bool sl, bool ld, uint32_t &ua, uint32_t &ub, uin
 /* Samples T and T + 1 (T even) of both channels: one window peek, one cursor advance and one
  * ring read per channel for two codewords (st_fused_step does one of each per codeword), then
  * the two restores in order. */
-template <int T, int FMT>
+template <int T, int FMT, int AS = -1>
 DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
                        uint32_t nq, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al,
                        uint32_t bs, bool store, u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1,
@@ -3403,16 +3450,19 @@ DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
     const uint32_t laneb = lane << 4;
     st_adv_nc(z0.b, n0, laneb);
     st_adv_nc(z1.b, n1, laneb);
-    /* the word read now and the one the next pair may read must have landed */
-    const bool ld0 = z0.b.wi >= z0.b.vlim, ld1 = z1.b.wi >= z1.b.vlim;
+    /* checked at every other pair (T = 0, 4): the word read now (read again after a landing)
+     * and the one the next pair reads must have landed; that pair moves wi by at most one,
+     * and the pair after it checks its own word again */
+    constexpr bool CHK = (T & 2) == 0;
+    const bool ld0 = CHK && z0.b.wi >= z0.b.vlim, ld1 = CHK && z1.b.wi >= z1.b.vlim;
     st_next_word(z0.b);
     st_next_word(z1.b);
     if (__builtin_expect(any_lane(sl0 || sl1 || ld0 || ld1), 0)) {
         st_rare_pair(z0, sl0, ld0, u0a, u0b, limit, trunc, nqt, lane);
         st_rare_pair(z1, sl1, ld1, u1a, u1b, limit, trunc, nqt, lane);
     }
-    st_lpc_out<T, FMT>(z0, z1, u0a, u1a, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
-    st_lpc_out<T + 1, FMT>(z0, z1, u0b, u1b, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
+    st_lpc_out<T, FMT, AS>(z0, z1, u0a, u1a, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
+    st_lpc_out<T + 1, FMT, AS>(z0, z1, u0b, u1b, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
 #if BNF_ST_CRC_PAIRS
     /* one in-ring CRC step per pair, channels alternating: independent of the decode chain */
     StCh &zc = ((T >> 1) & 1) ? z1 : z0;
@@ -3518,6 +3568,11 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     const bool anyw = any_lane(ok && (z0.wasted | z1.wasted) != 0u);
     const uint32_t as_u = __builtin_amdgcn_readfirstlane(as);
     const bool as_uni = !any_lane(ok && as != as_u);
+    /* the fused chunks' compile-time assignment: one per wave, no wasted bits (BNF_ST_ASFIX=0: off) */
+#ifndef BNF_ST_ASFIX
+#define BNF_ST_ASFIX 1
+#endif
+    const int as_fix = (BNF_ST_ASFIX && as_uni && !anyw && as_u <= 3u) ? (int)as_u : -1;
     const uint32_t fl_unit = lane & 3u; /* the flush: this lane's 16-byte unit of a frame's 64-byte run */
     const bool podd = (lane & 1u) != 0, phi = (lane & 2u) != 0;
 
@@ -3569,22 +3624,34 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                 st_pre2<7>(z0, z1, pre0, pre1); /* older taps of the chunk's first sample */
                 st_resync(z0.b, lane);
                 st_resync(z1.b, lane);
+                /* the chunk's 4 groups of 8 samples; AS >= 0: the wave's one assignment, no
+                 * wasted bits (st_decor4t), compiled per assignment */
+                auto chunk = [&](auto as_c) {
+                    constexpr int AS = decltype(as_c)::value;
 #pragma unroll 1
-                for (uint32_t g = 0; g < ST_CHK / 8; g++) {
-                    int32_t L[4], R[4];
-                    const uint32_t nq = nst + (STG ? 0u : g * 2u * ST_SPG); /* stores issued since the DMAs (at least) */
-                    const uint32_t nb = n0 + g * 8u;
-                    const bool sto = !(ablate & 2u);
+                    for (uint32_t g = 0; g < ST_CHK / 8; g++) {
+                        int32_t L[4], R[4];
+                        const uint32_t nq = nst + (STG ? 0u : g * 2u * ST_SPG); /* stores issued since the DMAs (at least) */
+                        const uint32_t nb = n0 + g * 8u;
+                        const bool sto = !(ablate & 2u);
 #if BNF_ST_PAIR
-#define FPAIR(T) st_fused_pair<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw, CT)
-                    FPAIR(0); FPAIR(2); FPAIR(4); FPAIR(6);
+#define FPAIR(T) st_fused_pair<T, FMT, AS>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw, CT)
+                        FPAIR(0); FPAIR(2); FPAIR(4); FPAIR(6);
 #undef FPAIR
 #else
 #define FSTEP(T) st_fused_step<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
-                    FSTEP(0); FSTEP(1); FSTEP(2); FSTEP(3); FSTEP(4); FSTEP(5); FSTEP(6); FSTEP(7);
+                        FSTEP(0); FSTEP(1); FSTEP(2); FSTEP(3); FSTEP(4); FSTEP(5); FSTEP(6); FSTEP(7);
 #undef FSTEP
 #endif
-                    if (STG && g == 0) { pk01[0] = pk[0]; pk01[1] = pk[1]; }
+                        if (STG && g == 0) { pk01[0] = pk[0]; pk01[1] = pk[1]; }
+                    }
+                };
+                switch (as_fix) {
+                case 0: chunk(std::integral_constant<int, 0>()); break;
+                case 1: chunk(std::integral_constant<int, 1>()); break;
+                case 2: chunk(std::integral_constant<int, 2>()); break;
+                case 3: chunk(std::integral_constant<int, 3>()); break;
+                default: chunk(std::integral_constant<int, -1>()); break;
                 }
                 z0.left -= ST_CHK;
                 z1.left -= ST_CHK;
@@ -3730,7 +3797,423 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         atomicAdd(&g_stats[12], (unsigned long long)(t_end - t_loopend));
     }
 }
-#endif /* BNF_TU == 3 || BNF_TU == 4 */
+
+#if BNF_TU == 7
+/* ============================================================ k_decode_sw
+ * One lane per stereo frame above 16 bits (C3: 96 kHz / 24-bit, M/S, wasted bits, LPC-12),
+ * k_decode_st's design with libFLAC's wide restore (lpc_restore_signal_wide @0x10006120):
+ * - two cursors per lane (one per subframe) on the same 8-slot LDS-DMA rings, refilled in
+ *   64-byte groups once per 32-sample chunk (st_refill_issue), one Rice codeword per channel
+ *   per step (C3's ~12.6-bit codewords: a pair overruns a 32-bit window on ~1% of lanes, which
+ *   would send ~3 of 4 wave steps down the rare path);
+ * - the exact predictor: Sum c[j] * x[n-1-j] in 64 bits (v_mad_i64_i32), the 11 older taps of
+ *   the next sample summed while the current one is decoded (two chains), so one MAC sits
+ *   between consecutive samples; libFLAC's 64-bit path keeps (int32)(S >> shift) (one
+ *   v_alignbit for shift < 32), the 32-bit paths (ia32, FIXED) ((int32)S) >> shift;
+ * - wasted bits, decorrelation and the output layout in registers: FLACFileReader's 3-byte
+ *   LE pack (FLACFileReader.cs:230-237) as v_perm words, 48 bytes per 8 stereo samples in
+ *   three 16-byte stores; interleaved / planar int32 in four;
+ * - tail as k_decode_st: zero padding, CRC-16 footer, the frame's CRC-16 from the LDS field
+ *   tables, zero-fill on mismatch (@0x10011af5).
+ * Frames it declines (MMX16 path, orders above 12, CONSTANT / VERBATIM, a 64-bit shift of 32 or
+ * more, errors, truncation) get BNF_FL_REDO and k_decode<16> decodes them from scratch. */
+#define SW_TAPS 12
+struct StW {
+    BR b;
+    int32_t c[SW_TAPS]; /* coefficients, 0 past the order (FIXED order o as LPC, shift 0) */
+    int32_t x[16];      /* history ring: x[n & 15] = sample n of the subframe */
+    int32_t sh;         /* shift of the libFLAC path (< 32) */
+    uint32_t wide;      /* 1: 64-bit path */
+    uint32_t k, km, k1, k32;
+    uint32_t esc, left, pidx, nparts, psamples, plen, pesc, porder, order;
+    uint32_t wasted;
+};
+
+DEV bool sw_setup(StW &z, uint32_t bps, uint32_t bs, uint64_t limit) {
+    SubHdr h;
+    int32_t warm[SW_TAPS], coef[SW_TAPS], err = -1;
+    const uint32_t st = parse_subframe_head<true, SW_TAPS>(z.b, bps, bs, limit, h, warm, coef, err);
+    if (st != BNF_ST_OK) return false;
+    if (h.type != T_FIXED && h.type != T_LPC) return false;
+    if (h.order > SW_TAPS) return false;
+    if (h.type == T_LPC && h.path == P_MMX16) return false;
+    if (h.type == T_LPC && h.path == P_WIDE && ((uint32_t)h.shift & 0xFFu) >= 32u) return false;
+#pragma unroll
+    for (int t = 0; t < SW_TAPS; t++) z.c[t] = (h.type == T_LPC && (uint32_t)t < h.order) ? coef[t] : 0;
+    if (h.type == T_FIXED) { /* FIXED order o: 1 | 2,-1 | 3,-3,1 | 4,-6,4,-1 (@0x10003810, 32-bit wrap) */
+        const uint32_t o = h.order;
+        z.c[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
+        z.c[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
+        z.c[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
+        z.c[3] = o == 4 ? -1 : 0;
+    }
+#pragma unroll
+    for (int t = 0; t < 16; t++) z.x[t] = (t < SW_TAPS && (uint32_t)t < h.order) ? warm[t < SW_TAPS ? t : 0] : 0;
+    z.wide = (h.type == T_LPC && h.path == P_WIDE) ? 1u : 0u;
+    z.sh = h.type == T_LPC ? (int32_t)((uint32_t)h.shift & (z.wide ? 0xFFu : 31u)) : 0;
+    z.order = h.order;
+    z.wasted = h.wasted;
+    z.porder = h.porder;
+    z.nparts = 1u << h.porder;
+    z.psamples = h.porder ? bs >> h.porder : bs - h.order;
+    z.plen = h.rice2 ? 5u : 4u;
+    z.pesc = h.rice2 ? 31u : 15u;
+    z.left = 0;
+    z.pidx = 0;
+    z.esc = 0;
+    z.k = 0;
+    z.km = 31;
+    z.k1 = 1;
+    z.k32 = 32;
+    return true;
+}
+
+/* c * x + acc exactly: one v_mad_i64_i32, written out.  With the coefficients loop-invariant
+ * the compiler hoisted their sign extension out of the chunk loop and then emitted full
+ * 64x64-bit multiplies (mad_u64_u32 + 2 mul_lo + add3); keeping the extension beside each
+ * multiply with an empty asm spilled (256 VGPRs). */
+DEV int64_t sw_mad(int32_t c, int32_t x, int64_t acc) {
+    int64_t d;
+    uint64_t co;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(c), "v"(x), "v"(acc));
+    return d;
+}
+DEV int64_t sw_mul(int32_t c, int32_t x) {
+    int64_t d;
+    uint64_t co;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(co) : "v"(c), "v"(x));
+    return d;
+}
+/* the 11 older taps of sample n + 1 (n = T mod 16): Sum_{j=1..11} c[j] * x[n - j], two chains
+ * (oldest taps first) */
+template <int T>
+DEV int64_t sw_pre(const StW &z) {
+    int64_t s0 = sw_mul(z.c[11], z.x[(T - 11 + 32) & 15]), s1 = sw_mul(z.c[10], z.x[(T - 10 + 32) & 15]);
+#pragma unroll
+    for (int j = 9; j >= 1; j--) {
+        if (j & 1) s0 = sw_mad(z.c[j], z.x[(T - j + 32) & 15], s0);
+        else s1 = sw_mad(z.c[j], z.x[(T - j + 32) & 15], s1);
+    }
+    return s0 + s1;
+}
+/* the path's prediction from the exact sum; PATH 0: every channel of the wave takes the
+ * 64-bit path, 2: per channel */
+template <int PATH>
+DEV int32_t sw_shift(const StW &z, int64_t S) {
+    const uint32_t lo = (uint32_t)S, hi = (uint32_t)((uint64_t)S >> 32);
+    const int32_t w = (int32_t)__builtin_amdgcn_alignbit(hi, lo, (uint32_t)z.sh); /* (int32)(S >> sh), sh < 32 */
+    if (PATH == 0) return w;
+    return z.wide ? w : ((int32_t)lo >> z.sh);
+}
+/* the full prediction of sample n (T = n mod 16), general path */
+template <int T, int PATH>
+DEV int32_t sw_full(const StW &z) {
+    return sw_shift<PATH>(z, sw_mad(z.c[0], z.x[(T + 15) & 15], sw_pre<(T + 15) & 15>(z)));
+}
+
+template <int AS>
+DEV void sw_decor(uint32_t as, int32_t &l, int32_t &r) {
+    if (AS < 0) decorrelate(as, l, r);
+    else decorrelate((uint32_t)AS, l, r);
+}
+
+/* 8 stereo samples n..n+7 of this lane's frame (nv valid) into the layout; al: 16-byte
+ * aligned runs (then 3 or 4 16-byte stores).  Returns whether the aligned path stored. */
+template <int FMT>
+DEV bool sw_emit8(uint8_t *dst, uint32_t n, uint32_t nv, bool al, uint32_t bs, const int32_t (&L)[8], const int32_t (&R)[8]) {
+    if (nv == 0) return false;
+    if (FMT == BNF_OUT_FILEREADER) { /* 24-bit LE, L R L R ... */
+        uint32_t d[12];
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const uint32_t l0 = (uint32_t)L[2 * h], r0 = (uint32_t)R[2 * h], l1 = (uint32_t)L[2 * h + 1], r1 = (uint32_t)R[2 * h + 1];
+            d[3 * h] = __builtin_amdgcn_perm(r0, l0, 0x04020100u);     /* l0.b0 l0.b1 l0.b2 r0.b0 */
+            d[3 * h + 1] = __builtin_amdgcn_perm(l1, r0, 0x05040201u); /* r0.b1 r0.b2 l1.b0 l1.b1 */
+            d[3 * h + 2] = __builtin_amdgcn_perm(r1, l1, 0x06050402u); /* l1.b2 r1.b0 r1.b1 r1.b2 */
+        }
+        uint8_t *o = dst + (uint64_t)n * 6u;
+        if (al && nv == 8) {
+#pragma unroll
+            for (int u = 0; u < 3; u++)
+                gst128((uint64_t)(uintptr_t)(o + 16 * u), u32x4{d[4 * u], d[4 * u + 1], d[4 * u + 2], d[4 * u + 3]});
+            return true;
+        }
+        const uint32_t nb = nv * 6u;
+        if ((((uintptr_t)o) & 3u) == 0) {
+            for (uint32_t i = 0; i < nb / 4u; i++) ((uint32_t *)o)[i] = d[i];
+            if (nb & 3u) { /* nv odd: two bytes of the last word */
+                const uint32_t v = d[nb / 4u];
+                o[nb - 2] = (uint8_t)v;
+                o[nb - 1] = (uint8_t)(v >> 8);
+            }
+        } else {
+            for (uint32_t i = 0; i < nb; i++) o[i] = (uint8_t)(d[i >> 2] >> (8u * (i & 3u)));
+        }
+        return false;
+    } else if (FMT == BNF_OUT_INTERLEAVED32) {
+        int32_t *o = (int32_t *)(dst + (uint64_t)n * 8u);
+        if (al && nv == 8) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) *(int4 *)(o + 4 * u) = make_int4(L[2 * u], R[2 * u], L[2 * u + 1], R[2 * u + 1]);
+            return true;
+        }
+        for (uint32_t q = 0; q < nv; q++) { o[2 * q] = L[q]; o[2 * q + 1] = R[q]; }
+        return false;
+    } else { /* PLANAR32 */
+        int32_t *o0 = (int32_t *)dst + n, *o1 = (int32_t *)dst + bs + n;
+        if (al && nv == 8) {
+            *(int4 *)o0 = make_int4(L[0], L[1], L[2], L[3]);
+            *(int4 *)(o0 + 4) = make_int4(L[4], L[5], L[6], L[7]);
+            *(int4 *)o1 = make_int4(R[0], R[1], R[2], R[3]);
+            *(int4 *)(o1 + 4) = make_int4(R[4], R[5], R[6], R[7]);
+            return true;
+        }
+        for (uint32_t q = 0; q < nv; q++) { o0[q] = L[q]; o1[q] = R[q]; }
+        return false;
+    }
+}
+template <int FMT> constexpr uint32_t sw_stores8() { return FMT == BNF_OUT_FILEREADER ? 3u : 4u; }
+
+/* One sample of both channels on the fused path (T = n mod 16): a Rice codeword per channel
+ * (k_decode_st's single step), the prediction from the older-tap sum of the previous step
+ * plus the newest tap, the next sample's older taps, the history, and at T = 7 / 15 the 8
+ * samples' wasted bits, decorrelation and stores. */
+template <int T, int FMT, int PATH, int AS>
+DEV void sw_fused_step(StW &z0, StW &z1, int32_t (&L)[8], int32_t (&R)[8], uint64_t limit, uint32_t &trunc, uint32_t nq,
+                       uint32_t as, uint8_t *dst, uint32_t nbase, bool al, uint32_t bs, bool sto, int64_t &pre0,
+                       int64_t &pre1, uint32_t lane) {
+    const int32_t p0 = sw_shift<PATH>(z0, sw_mad(z0.c[0], z0.x[(T + 15) & 15], pre0));
+    const int32_t p1 = sw_shift<PATH>(z1, sw_mad(z1.c[0], z1.x[(T + 15) & 15], pre1));
+    pre0 = sw_pre<T>(z0);
+    pre1 = sw_pre<T>(z1);
+    const uint32_t w0 = br_peek(z0.b), w1 = br_peek(z1.b);
+    const uint32_t q0 = ffbh(w0), q1 = ffbh(w1); /* ~0u for an empty window: slow */
+    const bool sl0 = q0 >= z0.k32, sl1 = q1 >= z1.k32;
+    uint32_t u0 = (q0 << z0.k) | __builtin_amdgcn_ubfe(w0, z0.km - q0, z0.k);
+    uint32_t u1 = (q1 << z1.k) | __builtin_amdgcn_ubfe(w1, z1.km - q1, z1.k);
+    const uint32_t laneb = lane << 4;
+    st_adv_nc(z0.b, sl0 ? 0u : q0 + z0.k1, laneb);
+    st_adv_nc(z1.b, sl1 ? 0u : q1 + z1.k1, laneb);
+    /* landing check on even steps: the word read now and the one the next step reads */
+    const bool ld0 = (T & 1) == 0 && z0.b.wi >= z0.b.vlim, ld1 = (T & 1) == 0 && z1.b.wi >= z1.b.vlim;
+    st_next_word(z0.b);
+    st_next_word(z1.b);
+    if (__builtin_expect(any_lane(sl0 || sl1 || ld0 || ld1), 0)) {
+        st_rare(z0, sl0, ld0, u0, limit, trunc, nq, lane);
+        st_rare(z1, sl1, ld1, u1, limit, trunc, nq, lane);
+    }
+    const int32_t s0 = (int32_t)(((u0 >> 1) ^ (0u - (u0 & 1u))) + (uint32_t)p0);
+    const int32_t s1 = (int32_t)(((u1 >> 1) ^ (0u - (u1 & 1u))) + (uint32_t)p1);
+    z0.x[T] = s0;
+    z1.x[T] = s1;
+    L[T & 7] = (int32_t)((uint32_t)s0 << z0.wasted);
+    R[T & 7] = (int32_t)((uint32_t)s1 << z1.wasted);
+    if ((T & 7) == 7) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) sw_decor<AS>(as, L[q], R[q]);
+        if (sto) sw_emit8<FMT>(dst, nbase + (uint32_t)T - 7u, 8u, al, bs, L, R);
+    }
+}
+
+/* One sample of both channels on the general path (warm-up, partition headers, escapes, the
+ * last partial chunk).  At T = 7 / 15 returns whether the aligned store path ran. */
+template <int T, int FMT>
+DEV bool sw_gen_step(StW &z0, StW &z1, int32_t (&L)[8], int32_t (&R)[8], uint64_t limit, uint32_t &trunc, uint32_t nst,
+                     uint32_t as, uint8_t *dst, uint32_t n, bool valid, bool al, uint32_t bs, bool sto) {
+    const bool v = valid && n < bs;
+    int32_t s0 = 0, s1 = 0;
+    if (v) {
+        if (n < z0.order) s0 = z0.x[T];
+        else s0 = (int32_t)((uint32_t)st_next(z0, limit, trunc, nst) + (uint32_t)sw_full<T, 2>(z0));
+        if (n < z1.order) s1 = z1.x[T];
+        else s1 = (int32_t)((uint32_t)st_next(z1, limit, trunc, nst) + (uint32_t)sw_full<T, 2>(z1));
+        z0.x[T] = s0;
+        z1.x[T] = s1;
+    }
+    L[T & 7] = (int32_t)((uint32_t)s0 << z0.wasted);
+    R[T & 7] = (int32_t)((uint32_t)s1 << z1.wasted);
+    bool stored = false;
+    if ((T & 7) == 7) {
+        const uint32_t nq = n - 7u;
+        const uint32_t nv = (valid && nq < bs) ? min(8u, bs - nq) : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; q++) decorrelate(as, L[q], R[q]);
+        if (sto) stored = sw_emit8<FMT>(dst, nq, nv, al, bs, L, R);
+    }
+    return stored;
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict__ words, uint64_t nbytes,
+                                                     uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
+                                                     uint8_t *__restrict__ out, uint64_t out_bytes,
+                                                     bnf_frame_info *__restrict__ info,
+                                                     const uint32_t *__restrict__ perm, uint32_t ablate) {
+    constexpr uint32_t SPG = sw_stores8<FMT>();
+    /* 16 KB: both channels' bitstream rings; in the tail, the 20 KB CRC-16 field tables */
+    __shared__ LDS_DMA_ALIGN uint32_t ring[(2 * ST_RD * RING_LANE_DW > CRC11_N / 2) ? 2 * ST_RD * RING_LANE_DW : CRC11_N / 2];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t slot = blockIdx.x * 64u + lane;
+    const uint32_t f = (perm && slot < nframes) ? perm[slot] : slot;
+    const uint64_t limit = nbytes * 8u;
+    bnf_frame_info fi;
+    const bool have = f < nframes;
+    if (have) fi = info[f];
+    const bool mine = have && fi.status == BNF_ST_OK && (fi.flags & BNF_FL_SW) && !(fi.flags & BNF_FL_REDO) &&
+                      (!(ablate & BNF_MODE_WREDO) || (fi.flags & BNF_FL_WAVE_REDO));
+    if (!__any(mine)) return;
+
+    uint64_t stride = 8;
+    bool ok = mine && fi.channels == 2 && chn_lanes >= 2 && sp.channels == 2;
+    if (FMT == BNF_OUT_FILEREADER) { stride = 6; ok = ok && sp.bps == 24; }
+    const uint32_t bs = ok ? fi.blocksize : 0u;
+    const uint64_t os = ok ? fi.out_sample : 0u;
+    ok = ok && (os + bs) * stride <= out_bytes;
+    uint8_t *dst = out + os * stride;
+    const bool al = (((uintptr_t)dst) & 15u) == 0 && (FMT != BNF_OUT_PLANAR32 || (bs & 3u) == 0);
+    const bool all_al = !any_lane(ok && !al); /* every run of the wave takes the 16-byte stores */
+
+    StW z0, z1;
+    lds_u32 *ring0 = (lds_u32 *)ring, *ring1 = (lds_u32 *)ring + ST_RD * RING_LANE_DW;
+    br_init(z0.b, words, nbytes, ring0, lane, ST_RD);
+    br_init(z1.b, words, nbytes, ring1, lane, ST_RD);
+    if (ok) {
+        br_seek(z0.b, fi.frame_off * 8u + fi.sub_start[0]);
+        ok = sw_setup(z0, sub_bps(fi, 0), bs, limit);
+    }
+    if (ok) {
+        br_seek(z1.b, fi.frame_off * 8u + fi.sub_start[1]);
+        ok = sw_setup(z1, sub_bps(fi, 1), bs, limit);
+    }
+    const uint32_t as = ok ? fi.assignment : 0u;
+    const uint32_t as_u = __builtin_amdgcn_readfirstlane(as);
+    const bool as_uni = !any_lane(ok && as != as_u);
+    const bool all_wide = !any_lane(ok && !(z0.wide && z1.wide));
+#ifndef BNF_SW_FIX
+#define BNF_SW_FIX 1
+#endif
+    /* the fused chunks' compile-time variant: the 64-bit path everywhere and one assignment,
+     * M/S (C3) or independent; anything else runs the per-lane variant */
+    const int fix = (BNF_SW_FIX && as_uni && all_wide && as_u <= 3u) ? (int)as_u : -1;
+
+    uint32_t mybs = ok ? bs : 0u;
+    for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
+    const uint32_t nchunks = (mybs + ST_CHK - 1) / ST_CHK;
+    uint32_t trunc = 0;
+    wait_vm(); /* setup loads done: the store count starts from zero */
+    uint32_t nst = 0; /* vector-memory ops (PCM stores) issued by this wave since the last refill's DMAs (a lower bound) */
+    for (uint32_t kc = 0; kc < nchunks; kc++) {
+        const uint32_t n0 = kc * ST_CHK;
+        const bool valid = ok && n0 < bs;
+        bool fast = valid && n0 >= 16u && n0 + ST_CHK <= bs && !(ablate & 12u);
+        if (fast) { /* partition headers at the chunk boundary (aligned partitions) */
+            if (z0.left == 0 && z0.pidx < z0.nparts) st_partition(z0);
+            if (z1.left == 0 && z1.pidx < z1.nparts) st_partition(z1);
+            fast = !z0.esc && !z1.esc && z0.left >= ST_CHK && z1.left >= ST_CHK;
+        }
+        const bool fused = !any_lane(valid && !fast);
+        const bool sto = !(ablate & 2u);
+        if (fused) {
+            if (valid) {
+                int64_t pre0 = sw_pre<15>(z0), pre1 = sw_pre<15>(z1); /* older taps of the chunk's first sample */
+                st_resync(z0.b, lane);
+                st_resync(z1.b, lane);
+                auto chunk = [&](auto pc, auto ac) {
+                    constexpr int PATH = decltype(pc)::value, AS = decltype(ac)::value;
+#pragma unroll 1
+                    for (uint32_t h = 0; h < ST_CHK / 16; h++) {
+                        int32_t L[8], R[8];
+                        const uint32_t nb = n0 + h * 16u;
+                        const uint32_t nqa = nst + (all_al && sto ? h * 2u * SPG : 0u);
+                        const uint32_t nqb = nqa + (all_al && sto ? SPG : 0u);
+#define SWS(T, NQ) sw_fused_step<T, FMT, PATH, AS>(z0, z1, L, R, limit, trunc, NQ, as, dst, nb, al, bs, sto, pre0, pre1, lane)
+                        SWS(0, nqa); SWS(1, nqa); SWS(2, nqa); SWS(3, nqa); SWS(4, nqa); SWS(5, nqa); SWS(6, nqa); SWS(7, nqa);
+                        SWS(8, nqb); SWS(9, nqb); SWS(10, nqb); SWS(11, nqb); SWS(12, nqb); SWS(13, nqb); SWS(14, nqb); SWS(15, nqb);
+#undef SWS
+                    }
+                };
+                if (fix == 3) chunk(std::integral_constant<int, 0>(), std::integral_constant<int, 3>());
+                else if (fix == 0) chunk(std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
+                else chunk(std::integral_constant<int, 2>(), std::integral_constant<int, -1>());
+                z0.left -= ST_CHK;
+                z1.left -= ST_CHK;
+            }
+            if (all_al && sto && any_lane(valid)) nst += (ST_CHK / 8) * SPG;
+        } else {
+#pragma unroll 1
+            for (uint32_t h = 0; h < ST_CHK / 16; h++) {
+                int32_t L[8], R[8];
+                const uint32_t nb = n0 + h * 16u;
+                bool st0, st1;
+#define SWG(T) sw_gen_step<T, FMT>(z0, z1, L, R, limit, trunc, nst, as, dst, nb + T, valid, al, bs, sto)
+                SWG(0); SWG(1); SWG(2); SWG(3); SWG(4); SWG(5); SWG(6);
+                st0 = SWG(7);
+                if (any_lane(st0)) nst += SPG;
+                SWG(8); SWG(9); SWG(10); SWG(11); SWG(12); SWG(13); SWG(14);
+                st1 = SWG(15);
+                if (any_lane(st1)) nst += SPG;
+#undef SWG
+            }
+        }
+        /* refill: wait for the previous refill's DMAs (the stores since stay in flight), then
+         * issue the next groups */
+        {
+            const bool want = valid && n0 + ST_CHK < bs;
+            wait_vm_n(nst);
+            z0.b.vendw = z0.b.iend * 4u;
+            z1.b.vendw = z1.b.iend * 4u;
+            st_refill_issue(z0.b, want);
+            st_refill_issue(z1.b, want);
+            nst = 0;
+        }
+    }
+
+    /* ---- end of the last subframe, zero padding, CRC-16 (read_frame_ tail) */
+    uint32_t crc_read = 0;
+    uint64_t end_byte = 0, resume = 0;
+    if (ok && trunc) ok = false;
+    if (ok) {
+        while (z1.pidx < z1.nparts) { /* finish_partitions */
+            const uint32_t kk = br_read(z1.b, z1.plen);
+            if (kk >= z1.pesc) br_read(z1.b, 5);
+            z1.pidx++;
+        }
+        const uint32_t padbits = (uint32_t)((8u - (br_pos(z1.b) & 7u)) & 7u);
+        const uint32_t zp = br_read(z1.b, padbits);
+        if (br_pos(z1.b) > limit || zp != 0) ok = false;
+        end_byte = br_pos(z1.b) >> 3;
+        crc_read = br_read(z1.b, 16);
+        if (br_pos(z1.b) > limit) ok = false;
+        resume = br_pos(z1.b);
+    }
+    uint32_t crc = crc_read;
+    const bool defer = (ablate & BNF_MODE_DEFER_CRC) != 0; /* k_crc_join checks it */
+    bool need = false;
+    if (ok && !defer) {
+        const uint32_t cn = info[f].crc_next;
+        const bool pre = (cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && fi.frame_off + (cn & BNF_CN_LEN) == end_byte + 2u;
+        need = !pre && !(ablate & 1u);
+    }
+    if (any_lane(need)) {
+        wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
+        lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
+        for (uint32_t i = lane; i < CRC11_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
+        __syncthreads();
+        if (need) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
+    }
+    if (ok && crc != crc_read) ok = false;
+    if (ok) {
+        info[f].resume_bit = resume;
+        info[f].crc16_read = crc_read;
+        info[f].crc16_calc = defer ? 0u : crc;
+        info[f].crc_ok = defer ? 0u : 1u;
+        if (defer) info[f].flags = fi.flags | BNF_FL_CRC_DEFER;
+    } else if (mine) {
+        info[f].flags = fi.flags | BNF_FL_REDO;
+    }
+}
+#endif /* BNF_TU == 7 */
+#endif /* BNF_TU == 3 || BNF_TU == 4 || BNF_TU == 7 */
 
 /* ------------------------------------------------------------- host launchers */
 /* The library is built from this file three times (BNF_TU 0: sync scan + k_parse + shared
@@ -3843,6 +4326,46 @@ hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint
         break;
     }
 #endif
+    return hipGetLastError();
+}
+} /* extern "C" */
+#endif
+
+#if BNF_TU == 7
+extern "C" {
+hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
+    return upload_tables(crc8, crc16x8, xpow);
+}
+void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate = v; }
+hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
+    uint64_t v[16];
+    hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < 16; i++) out16[i] += v[i];
+    if (reset) {
+        static const uint64_t z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z);
+    }
+    return e;
+}
+/* stereo frames above 16 bits; launched before k_decode<8>/<16>/<32> (it hands frames back to k_decode<16>) */
+hipError_t bnf_launch_decode_sw_tu7(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
+                                    uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
+                                    const uint32_t *perm, uint32_t mode, hipStream_t s) {
+    const dim3 grid((nframes + 63) / 64);
+    const uint32_t ab = ablate_flags() | mode;
+    switch (fmt) {
+    case BNF_OUT_PLANAR32:
+        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_PLANAR32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        break;
+    case BNF_OUT_INTERLEAVED32:
+        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_INTERLEAVED32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        break;
+    case BNF_OUT_FILEREADER:
+        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_FILEREADER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 } /* extern "C" */
@@ -4243,6 +4766,8 @@ hipError_t bnf_launch_decode_tu3(const uint32_t *, uint64_t, uint32_t, bnf_strea
                                  uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_launch_decode_tu4(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
                                  uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
+hipError_t bnf_launch_decode_sw_tu7(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                    uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_upload_tables_tu5(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu5(uint32_t);
 hipError_t bnf_stats_tu5(uint64_t *, int);
@@ -4253,6 +4778,9 @@ hipError_t bnf_upload_tables_tu2(const uint8_t *, const uint16_t *, const uint16
 hipError_t bnf_upload_tables_tu6(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu6(uint32_t);
 hipError_t bnf_stats_tu6(uint64_t *, int);
+hipError_t bnf_upload_tables_tu7(const uint8_t *, const uint16_t *, const uint16_t *);
+void bnf_set_ablate_tu7(uint32_t);
+hipError_t bnf_stats_tu7(uint64_t *, int);
 size_t bnf_decode_wave_lds(uint32_t, uint32_t);
 hipError_t bnf_launch_decode_wave_tu6(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, int, uint8_t *, uint64_t,
                                       bnf_frame_info *, uint32_t, uint32_t, hipStream_t);
@@ -4273,6 +4801,7 @@ hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const
     if (e == hipSuccess) e = bnf_upload_tables_tu4(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu5(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu6(crc8, crc16x8, xpow);
+    if (e == hipSuccess) e = bnf_upload_tables_tu7(crc8, crc16x8, xpow);
     return e;
 }
 
@@ -4300,6 +4829,7 @@ void bnf_set_ablate(uint32_t v) {
     bnf_set_ablate_tu4(v);
     bnf_set_ablate_tu5(v);
     bnf_set_ablate_tu6(v);
+    bnf_set_ablate_tu7(v);
 }
 
 hipError_t bnf_stats(uint64_t *out16, int reset) {
@@ -4309,6 +4839,7 @@ hipError_t bnf_stats(uint64_t *out16, int reset) {
     if (e == hipSuccess) e = bnf_stats_tu3(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu5(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu6(out16, reset);
+    if (e == hipSuccess) e = bnf_stats_tu7(out16, reset);
     return e == hipSuccess ? bnf_stats_tu4(out16, reset) : e;
 }
 
@@ -4577,6 +5108,9 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
      * instance does nearly all the work; forking would only add the other instances'
      * early-exiting launches beside it (C3's k_decode<16>: 13.4 -> 15.0 ms) */
     const int fm = sp.bps > 16 ? 0 : decode_fork_mode();
+    /* stereo frames above 16 bits: k_decode_sw first (serial above 16 bits), the other
+     * instances then take only its hand-backs among them */
+    const bool sw = sp.bps > 16 && sp.bps <= 24 && fmt != BNF_OUT_FLACDECODER && !(ablate_flags() & BNF_ABLATE_NO_SW);
     std::unique_lock<std::mutex> lk(g_side_mu, std::defer_lock);
     SideQ *sq = nullptr;
     if (fm) {
@@ -4595,6 +5129,10 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         return r;
     };
     if (sq && fm == 2) e = fork();
+    if (sw) {
+        if (e == hipSuccess) e = bnf_launch_decode_sw_tu7(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+        mode |= BNF_MODE_SW;
+    }
     if (e == hipSuccess)
         e = fmt == BNF_OUT_FLACDECODER
                 ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s)

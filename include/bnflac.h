@@ -154,7 +154,11 @@ BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_bytes, uint
  * Output position of each frame: d_out_sample[i] if non-NULL, else the header's
  * sample number (frame number x STREAMINFO blocksize for fixed-blocksize streams) minus
  * base_sample.  Frames that would end past out_bytes are not written (status 3,
- * flags bit 1).  d_info receives one record per frame.  Asynchronous on hip_stream. */
+ * flags bit 1).  d_info receives one record per frame.  A frame whose status is not OK
+ * (a parse error or truncation inside a subframe: libFLAC writes nothing for it) leaves its
+ * output range unspecified: the lane kernels may have stored part of it before finding the
+ * error.  A CRC-16 mismatch is status OK with crc_ok 0 and a zero-filled frame, as libFLAC
+ * writes it.  Asynchronous on hip_stream. */
 BNFLAC_API int bnflac_decode_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
                                     const uint64_t *d_frame_offsets, uint32_t nframes,
                                     const bnflac_stream_params *sp, const uint64_t *d_out_sample,
