@@ -3872,29 +3872,41 @@ DEV bool sw_setup(StW &z, uint32_t bps, uint32_t bs, uint64_t limit) {
  * the compiler hoisted their sign extension out of the chunk loop and then emitted full
  * 64x64-bit multiplies (mad_u64_u32 + 2 mul_lo + add3); keeping the extension beside each
  * multiply with an empty asm spilled (256 VGPRs). */
+/* vdst early-clobber: the 64-bit result must not overlap a 32-bit source (LLVM's own
+ * constraint on V_MAD_I64_I32; a build whose allocator overlapped them decoded garbage) */
 DEV int64_t sw_mad(int32_t c, int32_t x, int64_t acc) {
     int64_t d;
     uint64_t co;
-    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(c), "v"(x), "v"(acc));
-    return d;
-}
-DEV int64_t sw_mul(int32_t c, int32_t x) {
-    int64_t d;
-    uint64_t co;
-    asm("v_mad_i64_i32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(co) : "v"(c), "v"(x));
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=&v"(d), "=&s"(co) : "v"(c), "v"(x), "v"(acc));
     return d;
 }
 /* the 11 older taps of sample n + 1 (n = T mod 16): Sum_{j=1..11} c[j] * x[n - j], two chains
- * (oldest taps first) */
+ * (oldest taps first), as one asm block: the compiler puts a wait state after every inline
+ * asm statement (it cannot see its hazards), so one statement per sum, not per MAC */
 template <int T>
 DEV int64_t sw_pre(const StW &z) {
-    int64_t s0 = sw_mul(z.c[11], z.x[(T - 11 + 32) & 15]), s1 = sw_mul(z.c[10], z.x[(T - 10 + 32) & 15]);
-#pragma unroll
-    for (int j = 9; j >= 1; j--) {
-        if (j & 1) s0 = sw_mad(z.c[j], z.x[(T - j + 32) & 15], s0);
-        else s1 = sw_mad(z.c[j], z.x[(T - j + 32) & 15], s1);
-    }
-    return s0 + s1;
+    static_assert(SW_TAPS == 12, "sw_pre is written out for 12 taps");
+#define XJ(j) z.x[(T - (j) + 32) & 15]
+    int64_t a, b;
+    uint64_t cc;
+    asm("v_mad_i64_i32 %0, %2, %3, %4, 0\n\t"
+        "v_mad_i64_i32 %1, %2, %5, %6, 0\n\t"
+        "v_mad_i64_i32 %0, %2, %7, %8, %0\n\t"
+        "v_mad_i64_i32 %1, %2, %9, %10, %1\n\t"
+        "v_mad_i64_i32 %0, %2, %11, %12, %0\n\t"
+        "v_mad_i64_i32 %1, %2, %13, %14, %1\n\t"
+        "v_mad_i64_i32 %0, %2, %15, %16, %0\n\t"
+        "v_mad_i64_i32 %1, %2, %17, %18, %1\n\t"
+        "v_mad_i64_i32 %0, %2, %19, %20, %0\n\t"
+        "v_mad_i64_i32 %1, %2, %21, %22, %1\n\t"
+        "v_mad_i64_i32 %0, %2, %23, %24, %0\n\t"
+        "v_lshl_add_u64 %0, %0, 0, %1"
+        : "=&v"(a), "=&v"(b), "=&s"(cc)
+        : "v"(z.c[11]), "v"(XJ(11)), "v"(z.c[10]), "v"(XJ(10)), "v"(z.c[9]), "v"(XJ(9)), "v"(z.c[8]), "v"(XJ(8)),
+          "v"(z.c[7]), "v"(XJ(7)), "v"(z.c[6]), "v"(XJ(6)), "v"(z.c[5]), "v"(XJ(5)), "v"(z.c[4]), "v"(XJ(4)),
+          "v"(z.c[3]), "v"(XJ(3)), "v"(z.c[2]), "v"(XJ(2)), "v"(z.c[1]), "v"(XJ(1)));
+#undef XJ
+    return a;
 }
 /* the path's prediction from the exact sum; PATH 0: every channel of the wave takes the
  * 64-bit path, 2: per channel */
@@ -3982,18 +3994,20 @@ template <int T, int FMT, int PATH, int AS>
 DEV void sw_fused_step(StW &z0, StW &z1, int32_t (&L)[8], int32_t (&R)[8], uint64_t limit, uint32_t &trunc, uint32_t nq,
                        uint32_t as, uint8_t *dst, uint32_t nbase, bool al, uint32_t bs, bool sto, int64_t &pre0,
                        int64_t &pre1, uint32_t lane) {
-    const int32_t p0 = sw_shift<PATH>(z0, sw_mad(z0.c[0], z0.x[(T + 15) & 15], pre0));
-    const int32_t p1 = sw_shift<PATH>(z1, sw_mad(z1.c[0], z1.x[(T + 15) & 15], pre1));
-    pre0 = sw_pre<T>(z0);
-    pre1 = sw_pre<T>(z1);
+    /* source order is issue order here (the compiler keeps its MAC asm blocks in place): the
+     * two cursor chains first, the MAC blocks between their dependent steps */
     const uint32_t w0 = br_peek(z0.b), w1 = br_peek(z1.b);
     const uint32_t q0 = ffbh(w0), q1 = ffbh(w1); /* ~0u for an empty window: slow */
     const bool sl0 = q0 >= z0.k32, sl1 = q1 >= z1.k32;
+    const int32_t p0 = sw_shift<PATH>(z0, sw_mad(z0.c[0], z0.x[(T + 15) & 15], pre0));
+    const int32_t p1 = sw_shift<PATH>(z1, sw_mad(z1.c[0], z1.x[(T + 15) & 15], pre1));
     uint32_t u0 = (q0 << z0.k) | __builtin_amdgcn_ubfe(w0, z0.km - q0, z0.k);
     uint32_t u1 = (q1 << z1.k) | __builtin_amdgcn_ubfe(w1, z1.km - q1, z1.k);
     const uint32_t laneb = lane << 4;
     st_adv_nc(z0.b, sl0 ? 0u : q0 + z0.k1, laneb);
+    pre0 = sw_pre<T>(z0);
     st_adv_nc(z1.b, sl1 ? 0u : q1 + z1.k1, laneb);
+    pre1 = sw_pre<T>(z1);
     /* landing check on even steps: the word read now and the one the next step reads */
     const bool ld0 = (T & 1) == 0 && z0.b.wi >= z0.b.vlim, ld1 = (T & 1) == 0 && z1.b.wi >= z1.b.vlim;
     st_next_word(z0.b);
