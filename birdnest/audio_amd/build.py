@@ -18,8 +18,8 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "lib")
 INCLUDE = os.path.join(ROOT, "include")
 
-HIP_SOURCES = [os.path.join(CSRC, "bnflac_kernels.hip"), os.path.join(CSRC, "bnflac_runtime.cpp"),
-               os.path.join(CSRC, "bnflac_reader.cpp")]
+HIP_SOURCES = [os.path.join(CSRC, "bnflac_kernels.hip"), os.path.join(CSRC, "bnflac_sys.hip"),
+               os.path.join(CSRC, "bnflac_runtime.cpp"), os.path.join(CSRC, "bnflac_reader.cpp")]
 HIP_HEADERS = [os.path.join(CSRC, "bnflac_device.h"), os.path.join(CSRC, "bnflac_md5.h"), os.path.join(INCLUDE, "bnflac.h"),
                os.path.join(INCLUDE, "FLAC_compat.h")]
 SYNTH_SOURCES = [os.path.join(CSRC, "synth", "bnflac_synth.c")]

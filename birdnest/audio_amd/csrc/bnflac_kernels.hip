@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 
@@ -110,6 +111,9 @@ DEV void gst128(uint64_t addr, u32x4 v) { *(__attribute__((address_space(1))) u3
  * it handed them back).  Host ablation bit BNF_ABLATE_NO_SW: do not launch it. */
 #define BNF_MODE_SW 0x8000u
 #define BNF_ABLATE_NO_SW 0x10000u
+/* Mode bit: k_decode_list -- the frames of a device list (k_decode_sys's hand-backs), every
+ * class, decoded by this instance (no class split, stereo fast-path frames included). */
+#define BNF_MODE_LIST 0x20000u
 
 /* ----------------------------------------------------------------- bit reader */
 #define RING_MAX 16       /* 16-byte slots per lane (k_parse and k_decode_st use 8) */
@@ -2140,11 +2144,14 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
     const uint64_t limit = nbytes * 8u;
 
     bnf_frame_info fi;
-    bool have = (fl < fpb) && (f < nframes);
+    bool have = (fl < fpb) && (slot < nframes);
     if (ablate & BNF_MODE_WREDO) have = have && (info[f].flags & BNF_FL_WAVE_REDO); /* after k_decode_wave: its hand-backs */
     /* k_decode_sw's frames (BNF_MODE_SW: it ran first) are this kernel's only once handed back */
     const bool sw_on = (ablate & BNF_MODE_SW) != 0;
-    if (MAXW != 8) { /* most blocks are not this instance's: leave on two words of the record */
+    const bool lst = (ablate & BNF_MODE_LIST) != 0; /* k_decode_list: every frame of the list is this instance's */
+    if (lst) {
+        if (!__any(have)) return;
+    } else if (MAXW != 8) { /* most blocks are not this instance's: leave on two words of the record */
         const uint32_t fl = have ? info[f].flags : 0u;
         const bool w = have && info[f].status == BNF_ST_OK && (fl & (BNF_FL_W16 | BNF_FL_W32)) && !(fl & BNF_FL_ST) &&
                        !(sw_on && (fl & BNF_FL_SW) && !(fl & BNF_FL_REDO));
@@ -2162,14 +2169,14 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
      * those are decoded by the W = 8 instance, which runs after k_decode_st on its stream.
      * The W = 16 and 32 instances run beside them on a second stream and never look at
      * ST frames (the ST bit is k_parse's and does not change; REDO may be being set). */
-    const bool st_frame = have && (fi.flags & BNF_FL_ST) && !(ablate & 0x400u);
+    const bool st_frame = have && (fi.flags & BNF_FL_ST) && !(ablate & 0x400u) && !lst;
     if (st_frame && (MAXW != 8 || !(fi.flags & BNF_FL_REDO))) have = false;
     if (have && sw_on && (fi.flags & BNF_FL_SW) && !(fi.flags & BNF_FL_REDO)) have = false;
     bool frame_ok = have && fi.status == BNF_ST_OK;
     /* one wave per workgroup: the W = 8, 16 and 32 instances split the blocks between them
      * by the widest class among the block's non-ST frames (k_parse's flags); the W = 8
      * instance also takes the handed-back ST frames of the other instances' blocks */
-    {
+    if (!lst) {
         const bool a32 = __any(frame_ok && !st_frame && (fi.flags & BNF_FL_W32)) != 0;
         const bool a16 = __any(frame_ok && !st_frame && (fi.flags & BNF_FL_W16)) != 0;
         const int cls = a32 ? 32 : (a16 ? 16 : 8);
@@ -2571,6 +2578,28 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
     }
     decode_block<MAXW, CHK, RD>(blockIdx.x, ring, lds, words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info,
                                 perm, ablate);
+}
+
+/* k_decode_sys's hand-backs: the frames of a device list (list[0] = count, list[4..] = frame
+ * indices), decoded from scratch by the exact lane kernel.  The count is only known on the
+ * device, so a small grid strides over the list's blocks (an empty list costs one load per
+ * workgroup). */
+template <int MAXW, int CHK, int RD>
+__global__ void __launch_bounds__(DEC_LANES, 2) k_decode_list(const uint32_t *__restrict__ words, uint64_t nbytes,
+                                                           bnf_stream_params sp, uint32_t chn_lanes, int fmt,
+                                                           uint8_t *__restrict__ out, uint64_t out_bytes,
+                                                           bnf_frame_info *__restrict__ info,
+                                                           const uint32_t *__restrict__ list, uint32_t ablate) {
+    __shared__ LDS_DMA_ALIGN uint32_t ring[RD * RING_LANE_DW];
+    __shared__ int32_t lds[CHK * RP];
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(list[0]);
+    const uint32_t fpb = DEC_LANES >> __builtin_ctz(chn_lanes);
+    const uint32_t nb = (cnt + fpb - 1u) / fpb;
+    for (uint32_t blk = blockIdx.x; blk < nb; blk += gridDim.x) {
+        decode_block<MAXW, CHK, RD>(blk, ring, lds, words, nbytes, cnt, sp, chn_lanes, fmt, out, out_bytes, info, list + 4,
+                                    ablate | BNF_MODE_LIST | BNF_MODE_WREDO);
+        __syncthreads();
+    }
 }
 
 #if BNF_TU == 0
@@ -4296,6 +4325,18 @@ hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint
                        fmt, out, out_bytes, info, perm, ablate_flags() | mode, seg);
     return hipGetLastError();
 }
+#if BNF_TU == 2
+/* k_decode_sys's hand-back list (W = 32: every order); nframes bounds the list */
+hipError_t bnf_launch_decode_list_tu2(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
+                                      uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
+                                      const uint32_t *list, uint32_t mode, hipStream_t s) {
+    const uint32_t fpb = DEC_LANES / chn_lanes;
+    const uint32_t nb = std::min<uint32_t>((nframes + fpb - 1) / fpb, 512u);
+    hipLaunchKernelGGL((k_decode_list<DEC_W, 32, DEC_RD>), dim3(std::max(nb, 1u)), dim3(DEC_LANES), 0, s, words, nbytes, sp,
+                       chn_lanes, fmt, out, out_bytes, info, list, ablate_flags() | mode);
+    return hipGetLastError();
+}
+#endif
 } /* extern "C" */
 #endif
 
@@ -4796,6 +4837,12 @@ hipError_t bnf_upload_tables_tu7(const uint8_t *, const uint16_t *, const uint16
 void bnf_set_ablate_tu7(uint32_t);
 hipError_t bnf_stats_tu7(uint64_t *, int);
 size_t bnf_decode_wave_lds(uint32_t, uint32_t);
+hipError_t bnf_upload_tables_tu8(const uint8_t *, const uint16_t *, const uint16_t *);
+void bnf_set_ablate_tu8(uint32_t);
+hipError_t bnf_launch_decode_sys_tu8(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                     uint64_t, bnf_frame_info *, const uint32_t *, uint32_t *, uint32_t, hipStream_t);
+hipError_t bnf_launch_decode_list_tu2(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                      uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_launch_decode_wave_tu6(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, int, uint8_t *, uint64_t,
                                       bnf_frame_info *, uint32_t, uint32_t, hipStream_t);
 void bnf_set_ablate_tu1(uint32_t);
@@ -4816,6 +4863,7 @@ hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const
     if (e == hipSuccess) e = bnf_upload_tables_tu5(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu6(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu7(crc8, crc16x8, xpow);
+    if (e == hipSuccess) e = bnf_upload_tables_tu8(crc8, crc16x8, xpow);
     return e;
 }
 
@@ -4844,6 +4892,7 @@ void bnf_set_ablate(uint32_t v) {
     bnf_set_ablate_tu5(v);
     bnf_set_ablate_tu6(v);
     bnf_set_ablate_tu7(v);
+    bnf_set_ablate_tu8(v);
 }
 
 hipError_t bnf_stats(uint64_t *out16, int reset) {
@@ -5039,7 +5088,24 @@ static bool use_decode_wave(uint32_t nframes, uint32_t cmax, uint32_t bsmax) {
     return DW_AUTO && nframes <= 2u * cus * wpc;
 }
 
+/* k_decode_sys (systolic restore, every frame class) or the lane kernels by class.
+ * BNFLAC_DECODE_SYS=0 never, 1 always; bnf_set_decode_sys overrides. */
+static std::atomic<int> g_decode_sys{-1};
+static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32_t chn_lanes) {
+    int m = g_decode_sys.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char *e = getenv("BNFLAC_DECODE_SYS");
+        m = e ? (atoi(e) ? 1 : 0) : 2;
+        g_decode_sys.store(m, std::memory_order_relaxed);
+    }
+    (void)nframes;
+    (void)sp;
+    if (chn_lanes > 8u) return false;
+    return m == 1;
+}
+
 extern "C" {
+void bnf_set_decode_sys(int mode) { g_decode_sys.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
 void bnf_set_decode_wave(int mode) { g_decode_wave = mode < 0 ? 2 : (mode ? 1 : 0); } /* -1: auto */
 void bnf_set_parse_wave(int mode) { g_parse_wave = mode < 0 ? 2 : (mode ? 1 : 0); } /* -1: auto */
 hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset) { /* debug counters of k_parse_wave (BNFLAC_PW_STATS=1) */
@@ -5089,6 +5155,19 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
                              uint32_t *order, hipEvent_t ev_crc, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
     uint32_t mode = ev_crc ? BNF_MODE_DEFER_CRC : 0u; /* a concurrent CRC pass is running (k_crc) */
+    /* every frame through k_decode_sys (decode order by class and blocksize), then its
+     * hand-backs through k_decode_list; order scratch: 256 + nframes (perm) + 4 + nframes (list) */
+    if (order && !ev_crc && use_decode_sys(nframes, sp, chn_lanes)) {
+        const uint32_t *perm = nullptr;
+        uint32_t *list = order + 256u + nframes;
+        hipError_t e = hipMemsetAsync(list, 0, 16, s);
+        if (e == hipSuccess) e = launch_order<0>(info, nullptr, 0, nullptr, nframes, order, &perm, s);
+        if (e == hipSuccess)
+            e = bnf_launch_decode_sys_tu8(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, list, mode, s);
+        if (e == hipSuccess)
+            e = bnf_launch_decode_list_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, list, mode, s);
+        return e;
+    }
     /* small launches: a wave per frame (k_decode_wave), then the lane kernels for its
      * hand-backs only (frames wider than STREAMINFO's bounds) */
     {

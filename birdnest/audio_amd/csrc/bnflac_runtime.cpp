@@ -153,9 +153,12 @@ extern "C" void bnf_set_parse_wave(int mode);
 /* parse kernel: -1 auto (k_parse_wave for small launches), 0 k_parse, 1 k_parse_wave (tests, A/B) */
 extern "C" BNFLAC_API void bnflac_debug_set_parse_wave(int mode) { bnf_set_parse_wave(mode); }
 extern "C" void bnf_set_decode_wave(int mode);
-/* decode kernels: -1 auto (k_decode_wave for small launches), 0 the lane kernels, 1 k_decode_wave
- * whenever the rows fit (tests, A/B) */
+/* k_decode_wave: -1 auto (DW_AUTO: currently never), 0 off, 1 whenever the rows fit (tests, A/B) */
 extern "C" BNFLAC_API void bnflac_debug_set_decode_wave(int mode) { bnf_set_decode_wave(mode); }
+extern "C" void bnf_set_decode_sys(int mode);
+/* k_decode_sys (systolic restore, every frame class): -1 auto (BNFLAC_DECODE_SYS), 0 the lane
+ * kernels by class, 1 always (tests, A/B) */
+extern "C" BNFLAC_API void bnflac_debug_set_decode_sys(int mode) { bnf_set_decode_sys(mode); }
 extern "C" hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset);
 /* k_parse_wave's debug counters (collected when BNFLAC_PW_STATS is set): passes, splice rounds,
  * serial fallbacks, partitions, frames, wave-cycles in scans.  out8: 8 values. */
@@ -319,7 +322,8 @@ extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d
     if (out_format < 0 || out_format > 3) return fail("bnflac_decode_parsed: bad out_format");
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
-    if (!ctx->order.grow(sizeof(uint32_t) * (256u + (size_t)nframes)))
+    /* decode order (256 + nframes) + k_decode_sys's hand-back list (4 + nframes) */
+    if (!ctx->order.grow(sizeof(uint32_t) * (260u + 2u * (size_t)nframes)))
         return fail("bnflac_decode_parsed: out of device memory (decode-order scratch)");
     /* the records of this call came from bnflac_parse_frames with the concurrent CRC pass:
      * the decode defers the check to k_crc_join after it */
