@@ -28,7 +28,8 @@ cpu_baseline = the CPU restatement (oracle/: libFLAC 1.2.1 decode + the C# pack 
                on a bounded sample of the same frames.
 
     python bench.py [--gpus N --steps K --warmup W --batches B --config C2|C3|C4|C5 --legs C3,C4,C5]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    torchrun --nproc-per-node N bench.py --gpus N ...   (or: python bench.py --gpus N, which starts the
+                                                         N rank processes itself)
 """
 from __future__ import annotations
 
@@ -71,7 +72,8 @@ CONFIGS = {
 
 def parse_args():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher (WORLD_SIZE unset) bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS), help="headline workload")
@@ -99,7 +101,83 @@ def parse_args():
     ap.add_argument("--ablate", default=None,
                     help="comma list of ablation bitmasks to time after the measurement (timing only, wrong output): "
                          "1 CRC, 2 stores, 4 restore, 8 rice, 16 parse walk")
+    ap.add_argument("--spawn-dry-run", action="store_true", help=argparse.SUPPRESS)  # print the rank plan (tests)
+    ap.add_argument("--rank-selftest", action="store_true", help=argparse.SUPPRESS)  # gloo all_reduce per rank (tests)
     return ap.parse_args()
+
+
+# --------------------------------------------------------------------------- rank launcher
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_plan(n: int, port: int) -> list:
+    """The environment of each of n rank processes on this node (torch.distributed.run's
+    variables; rendezvous on 127.0.0.1)."""
+    return [{"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+             "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)} for r in range(n)]
+
+
+def launch_ranks(args) -> int | None:
+    """`--gpus N` and the process count must agree.  Under a launcher (WORLD_SIZE set) a
+    mismatch is refused; without one, N > 1 starts the N rank processes here -- children, not
+    an exec, and before anything in this process touches the GPU -- and returns their exit
+    status (the first failure ends the others, so a dead rank cannot leave its peers waiting in
+    a collective).  None: this process is a rank (or the only one) and runs the bench."""
+    world_env = os.environ.get("WORLD_SIZE") or None
+    if world_env is not None:
+        if args.gpus is not None and int(world_env) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}: refusing a mismatched run",
+                  file=sys.stderr, flush=True)
+            return 2
+        return None
+    n = args.gpus or 1
+    if n <= 1:
+        return None
+    plan = rank_plan(n, _free_port())
+    if args.spawn_dry_run:
+        print(json.dumps({"ranks": plan, "argv": sys.argv[1:]}), flush=True)
+        return 0
+    import subprocess
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=dict(os.environ, **e))
+             for e in plan]
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:  # the exact children this launcher started
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def rank_selftest(args) -> None:
+    """One gloo all_reduce per rank (CPU): proves the launcher's rank environment."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"world": world, "sum": int(t.item()), "gpus": args.gpus,
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def affinity_cores() -> int:
@@ -481,14 +559,15 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
     d_offs = torch.from_numpy(np.concatenate(offs) if offs else np.zeros(0, np.int64)).to(dev)
     d_os = torch.from_numpy(np.concatenate(osmp) if osmp else np.zeros(0, np.int64)).to(dev)
     d_out = torch.empty(max(nsmp * stride, 1), dtype=torch.uint8, device=dev)
+    d_out2 = torch.empty_like(d_out)  # the overlapped flow's second output buffer
     d_info = torch.zeros(max(nframes, 1) * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     nb = int(base[-1])
 
-    def decode():
+    def decode(out=d_out):
         if nframes:
             dec.parse_frames(d_bytes, nb, d_offs, nframes, sp, d_info, d_out_sample=d_os, stream=stream)
-            dec.decode_parsed(d_bytes, nb, nframes, sp, fmt, d_out, d_info, stream=stream)
+            dec.decode_parsed(d_bytes, nb, nframes, sp, fmt, out, d_info, stream=stream)
 
     for _ in range(args.warmup):
         decode()
@@ -521,16 +600,46 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
     if world > 1:
         dist.barrier()
     t_all = time.perf_counter() - t0
+    # decode + gather, overlapped across steps: step s decodes into one of two output buffers
+    # and posts its gather (shard.gather_post: RCCL point-to-point ops ordered after that
+    # decode); step s + 1's decode into the other buffer runs while it is in flight, and a
+    # buffer is decoded into again only after its previous gather finished (work.wait)
+    t_ovl = t_all
+    gathered_ovl = None
     if world > 1:
-        t = torch.tensor([t_dec, t_all], dtype=torch.float64, device=dev)
+        nbytes_out = nsmp * stride
+        sizes = shard.gather_sizes(d_out[:nbytes_out])
+        bufs, pend, parts = [d_out, d_out2], [[], []], [None, None]
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for st in range(args.steps):
+            b = st % 2
+            for wk in pend[b]:
+                wk.wait()
+            decode(bufs[b])
+            pend[b], parts[b] = shard.gather_post(bufs[b][:nbytes_out], sizes, parts=parts[b])
+        for b in (0, 1):
+            for wk in pend[b]:
+                wk.wait()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t_ovl = time.perf_counter() - t0
+        last = (args.steps - 1) % 2
+        if rank == 0 and parts[last] is not None:
+            gathered_ovl = torch.cat(parts[last])
+    if world > 1:
+        t = torch.tensor([t_dec, t_all, t_ovl], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_dec, t_all = float(t[0].item()), float(t[1].item())
+        t_dec, t_all, t_ovl = float(t[0].item()), float(t[1].item()), float(t[2].item())
     ok = True
     if rank == 0:
         local = dict(zip(mine, streams))
         ref = b"".join(pack_reference((local[i] if i in local else synth.encode(synth.config("C5", seed=5 + 1000 * i))).pcm,
                                       "FILEREADER", 24) for i in range(F))
         ok = gathered is not None and gathered.cpu().numpy().tobytes() == ref
+        if world > 1:
+            ok = ok and gathered_ovl is not None and gathered_ovl.cpu().numpy().tobytes() == ref
     if world > 1:
         o = torch.tensor([1 if ok else 0], device=dev)
         dist.all_reduce(o, op=dist.ReduceOp.MIN)
@@ -542,8 +651,8 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
     samples = int(tot.item())
     comp = sum(len(s.data) - int(s.frame_offsets[0]) for s in streams)
     alg = comp + nsmp * stride
-    return {"samples": samples, "t_dec": t_dec, "t_all": t_all, "t_launch": t_launch, "ok": ok, "files": F,
-            "alg_bytes_rank": alg, "frames_rank": nframes}
+    return {"samples": samples, "t_dec": t_dec, "t_all": t_all, "t_ovl": t_ovl, "t_launch": t_launch, "ok": ok,
+            "files": F, "alg_bytes_rank": alg, "frames_rank": nframes}
 
 
 def c5_summary(r, args, world):
@@ -555,7 +664,11 @@ def c5_summary(r, args, world):
            "roofline": roofline(r["alg_bytes_rank"], r["t_launch"], 0.0, step_ms),
            "with_gather": {"value": round(r["samples"] * args.steps / r["t_all"] / 1e6, 2), "unit": "MSamples/s",
                            "ms_per_step": round(r["t_all"] / args.steps * 1e3, 4),
-                           "note": "each step: decode, then shard.gather_bytes of every rank's PCM to rank 0"}}
+                           "note": "each step: decode, then shard.gather_bytes of every rank's PCM to rank 0"},
+           "with_gather_overlapped": {"value": round(r["samples"] * args.steps / r["t_ovl"] / 1e6, 2),
+                                      "unit": "MSamples/s", "ms_per_step": round(r["t_ovl"] / args.steps * 1e3, 4),
+                                      "note": "step s's gather (shard.gather_post, RCCL send/recv) in flight while "
+                                              "step s + 1 decodes into a second buffer; N = 1: no gather"}}
     out["roofline"]["kernel"] = "k_parse + decode launch over the rank's files"
     return out
 
@@ -563,10 +676,18 @@ def c5_summary(r, args, world):
 # --------------------------------------------------------------------------- main
 def main():
     args = parse_args()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.rank_selftest:
+        rank_selftest(args)
+        return
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    assert args.gpus is None or args.gpus == world, "rank count differs from --gpus"
+    args.gpus = world
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -652,6 +773,10 @@ def main():
         w = max(1, int(buf[5]))
         line["stats"]["cycles_per_wave"] = {n: int(buf[8 + i]) // w for i, n in
                                             enumerate(["setup", "decode", "refill", "pack", "tail"])}
+        # k_decode_sys (BNFLAC_DECODE_SYS=1): s_memtime per producer wave / per restore wave
+        line["stats"]["sys_cycles"] = {n: int(buf[8 + i]) // w for i, n in
+                                       enumerate(["prod_refill", "prod_rice", "prod_barrier", "rest_steps",
+                                                  "rest_pack", "rest_barrier"])}
     if args.ablate and rank == 0:
         abl = []
         for m in [int(x, 0) for x in args.ablate.split(",")]:

@@ -4838,6 +4838,7 @@ void bnf_set_ablate_tu7(uint32_t);
 hipError_t bnf_stats_tu7(uint64_t *, int);
 size_t bnf_decode_wave_lds(uint32_t, uint32_t);
 hipError_t bnf_upload_tables_tu8(const uint8_t *, const uint16_t *, const uint16_t *);
+hipError_t bnf_stats_tu8(uint64_t *, int);
 void bnf_set_ablate_tu8(uint32_t);
 hipError_t bnf_launch_decode_sys_tu8(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
                                      uint64_t, bnf_frame_info *, const uint32_t *, uint32_t *, uint32_t, hipStream_t);
@@ -4903,6 +4904,7 @@ hipError_t bnf_stats(uint64_t *out16, int reset) {
     if (e == hipSuccess) e = bnf_stats_tu5(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu6(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu7(out16, reset);
+    if (e == hipSuccess) e = bnf_stats_tu8(out16, reset);
     return e == hipSuccess ? bnf_stats_tu4(out16, reset) : e;
 }
 

@@ -52,7 +52,8 @@
 #define SYS_RP 80                    /* row stride (dwords), [sample][slot]: 80 = 16 mod 64 banks */
 #define SYS_CW 4                     /* restore waves per workgroup (16 subframe slots each) */
 #define SYS_THREADS (64 * (1 + SYS_CW))
-#define SYS_RD 8                     /* producer ring: 16-byte blocks per lane */
+#define SYS_RD 16                    /* producer ring: 16-byte blocks per lane (256 B ahead of the cursor) */
+#define SYS_HALF 16                  /* producer step: residuals per refill and per fast run */
 #define SYS_CS 33                    /* coefficient table stride per slot (bank spread) */
 
 static_assert(SYS_CHK == 32, "the restore chunk is written for 32 samples (8 per quad lane)");
@@ -77,18 +78,29 @@ struct SysShared {
 };
 
 DEV void sys_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+/* debug phase timers (ablate 0x100, bench.py --stats): s_memtime, wave-uniform points only */
+DEV uint64_t sys_now(bool on) {
+    if (!on) return 0ull;
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return t;
+}
 
-/* 2-deep producer refill, every 16 samples: the blocks issued by the previous refill may stay in
- * flight; everything issued before it has landed (vmcnt retires in issue order and the producer
- * issues no other vector-memory ops).  Then the blocks up to SYS_RD past the cursor's block. */
+/* 4-deep producer refill, every SYS_HALF residuals: the DMAs of the last three refills may stay
+ * in flight (vmcnt retires in issue order and the producer issues no other vector-memory ops),
+ * everything issued before them has landed.  Then the blocks up to SYS_RD past the cursor's
+ * block.  d*: DMA instructions of the last refills (wave-uniform), e*: the lane's iend when
+ * each of them started (shift registers, so every index is a compile-time constant). */
 struct SysQ {
-    uint32_t d_last; /* DMA instructions of the previous refill (wave-uniform) */
-    uint32_t e1;     /* the lane's iend when the previous refill started */
+    uint32_t d0, d1, d2;
+    uint32_t e0, e1, e2;
 };
 DEV void sys_refill(BR &b, bool want, SysQ &q) {
-    wait_vm_n(q.d_last);
-    b.vendw = max(b.vendw, q.e1 * 4u);
-    q.e1 = b.iend;
+    wait_vm_n(q.d0 + q.d1 + q.d2);
+    b.vendw = max(b.vendw, q.e2 * 4u); /* issued before the refill three back: landed */
+    q.e2 = q.e1;
+    q.e1 = q.e0;
+    q.e0 = b.iend;
     const uint32_t cb = b.wi >> 2;
     const uint32_t lo = max(b.iend, cb), hi = cb + b.rdepth;
     uint32_t d = 0;
@@ -102,7 +114,97 @@ DEV void sys_refill(BR &b, bool want, SysQ &q) {
         }
     }
     if (want) b.iend = max(b.iend, hi);
-    q.d_last = d;
+    q.d2 = q.d1;
+    q.d1 = q.d0;
+    q.d0 = d;
+}
+
+/* ------------------------------------------------------------------ producer fast path */
+/* Ring byte address of word wi (bits 2-3 word in block, 4-9 lane, 10-13 slot), moved on one word
+ * by ((ra | 0x3F3) + c) & 0x3C0C | lane bits (k_decode_st's incremental form, 16 slots) */
+static_assert(SYS_RD == 16, "sys_adv's address arithmetic is written for 16 ring slots");
+DEV uint32_t sys_ra(uint32_t wi, uint32_t lane) { return ((wi & 3u) << 2) | (lane << 4) | (((wi >> 2) & 15u) << 10); }
+DEV void sys_adv(BR &b, uint32_t n, uint32_t laneb) { /* n <= 32, no landing check */
+    uint32_t t;
+    const bool c = __builtin_usub_overflow(b.s, n, &t);
+    b.s = t & 31u;
+    b.hi = c ? b.lo : b.hi;
+    b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
+    b.wi += (uint32_t)c;
+    b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x3C0Cu) | laneb;
+}
+DEV void sys_next_word(BR &b) { b.nx = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + b.ra); }
+DEV void sys_resync(BR &b, uint32_t lane) { b.ra = sys_ra(b.wi, lane); b.vlim = b.vendw - 1u; }
+DEV int32_t sys_zz(uint32_t u) { return (int32_t)((u >> 1) ^ (0u - (u & 1u))); }
+/* rare cases of a fast step: the cursor entered ring words not known to have landed (wait for
+ * every DMA, refill if still short, read the word again), or a codeword / pair too long for the
+ * window (this lane did not advance: decode it with the generic reader) */
+template <int NW>
+DEV void sys_rare(BR &b, bool sl, bool ld, uint32_t k, uint32_t (&u)[NW], uint64_t limit, uint32_t &trunc, uint32_t lane) {
+    if (any_lane(ld)) {
+        STAT(b.stats, 2);
+        wait_vm();
+        b.vendw = b.iend * 4u;
+        if (b.wi + 1u >= b.vendw) {
+            br_refill(b);
+            wait_vm();
+            br_drained(b);
+        }
+        sys_resync(b, lane);
+        sys_next_word(b);
+    }
+    if (any_lane(sl)) {
+        STAT(b.stats, 3);
+        if (sl) {
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
+                uint32_t qq;
+                if (!br_unary(b, qq, limit)) trunc = 1;
+                u[i] = (qq << k) | br_read(b, k);
+            }
+        }
+        sys_resync(b, lane);
+    }
+}
+/* SYS_HALF Rice codewords of one partition (parameter k; km = 31 - k, k1 = k + 1, k32 = 32 - k),
+ * unchecked except for a landing test every other step, into registers.  PAIR: two codewords per
+ * 32-bit window (small k: C2's ~10-bit codewords) with one advance and one ring read. */
+template <bool PAIR>
+DEV void sys_rice_run(BR &b, bool on, uint32_t k, uint32_t km, uint32_t k1, uint32_t k32, int32_t (&r)[SYS_HALF],
+                      uint64_t limit, uint32_t &trunc, uint32_t lane) { /* on: this lane decodes (others stand still) */
+    const uint32_t laneb = lane << 4;
+    sys_resync(b, lane);
+#pragma unroll
+    for (int T = 0; T < SYS_HALF; T += PAIR ? 2 : 1) {
+        const uint32_t w = br_peek(b);
+        if (PAIR) {
+            uint32_t u[2];
+            const uint32_t qa = min(ffbh(w), 32u);
+            const uint32_t la = qa + k1;
+            const uint32_t w2 = w << (la & 31u);
+            const uint32_t qb = min(ffbh(w2), 32u);
+            u[0] = (qa << k) | __builtin_amdgcn_ubfe(w, km - qa, k);
+            u[1] = (qb << k) | __builtin_amdgcn_ubfe(w2, km - qb, k);
+            const uint32_t n = la + qb + k1;
+            const bool sl = on && n > 32u;
+            sys_adv(b, (sl || !on) ? 0u : n, laneb);
+            const bool ld = on && (T & 2) == 0 && b.wi >= b.vlim;
+            sys_next_word(b);
+            if (__builtin_expect(any_lane(sl || ld), 0)) sys_rare<2>(b, sl, ld, k, u, limit, trunc, lane);
+            r[T] = sys_zz(u[0]);
+            r[T + 1] = sys_zz(u[1]);
+        } else {
+            uint32_t u[1];
+            const uint32_t q = ffbh(w); /* ~0u for an empty window: slow */
+            const bool sl = on && q >= k32;
+            u[0] = (q << k) | __builtin_amdgcn_ubfe(w, km - q, k);
+            sys_adv(b, (sl || !on) ? 0u : q + k1, laneb);
+            const bool ld = on && (T & 1) == 0 && b.wi >= b.vlim;
+            sys_next_word(b);
+            if (__builtin_expect(any_lane(sl || ld), 0)) sys_rare<1>(b, sl, ld, k, u, limit, trunc, lane);
+            r[T] = sys_zz(u[0]);
+        }
+    }
 }
 
 /* ------------------------------------------------------------------ the restore quad */
@@ -114,6 +216,44 @@ DEV int64_t sys_mad(int32_t c, int32_t x, int64_t acc) {
     uint64_t co;
     asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=&v"(d), "=&s"(co) : "v"(c), "v"(x), "v"(acc));
     return d;
+}
+/* acc[a] += c[a] * bc for a < A, exactly (v_mad_i64_i32), as ONE asm statement: the compiler
+ * puts a wait state after every inline asm statement it cannot see into */
+template <int A> DEV void sys_macs(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc);
+template <> DEV void sys_macs<1>(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+    uint64_t co;
+    asm("v_mad_i64_i32 %0, %1, %3, %2, %0"
+        : "+v"(acc[0]), "=&s"(co)
+        : "v"(bc), "v"(c[0]));
+}
+template <> DEV void sys_macs<2>(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+    uint64_t co;
+    asm("v_mad_i64_i32 %0, %2, %4, %3, %0\n\t"
+        "v_mad_i64_i32 %1, %2, %5, %3, %1"
+        : "+v"(acc[0]), "+v"(acc[1]), "=&s"(co)
+        : "v"(bc), "v"(c[0]), "v"(c[1]));
+}
+template <> DEV void sys_macs<4>(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+    uint64_t co;
+    asm("v_mad_i64_i32 %0, %4, %6, %5, %0\n\t"
+        "v_mad_i64_i32 %1, %4, %7, %5, %1\n\t"
+        "v_mad_i64_i32 %2, %4, %8, %5, %2\n\t"
+        "v_mad_i64_i32 %3, %4, %9, %5, %3"
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "=&s"(co)
+        : "v"(bc), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]));
+}
+template <> DEV void sys_macs<8>(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+    uint64_t co;
+    asm("v_mad_i64_i32 %0, %8, %10, %9, %0\n\t"
+        "v_mad_i64_i32 %1, %8, %11, %9, %1\n\t"
+        "v_mad_i64_i32 %2, %8, %12, %9, %2\n\t"
+        "v_mad_i64_i32 %3, %8, %13, %9, %3\n\t"
+        "v_mad_i64_i32 %4, %8, %14, %9, %4\n\t"
+        "v_mad_i64_i32 %5, %8, %15, %9, %5\n\t"
+        "v_mad_i64_i32 %6, %8, %16, %9, %6\n\t"
+        "v_mad_i64_i32 %7, %8, %17, %9, %7"
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7]), "=&s"(co)
+        : "v"(bc), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]));
 }
 /* lane j's broadcast of lane JJ of its quad (DPP quad_perm) */
 template <int JJ> DEV int32_t quad_bcast(int32_t x) { return __builtin_amdgcn_mov_dpp(x, JJ * 0x55, 0xF, 0xF, false); }
@@ -133,7 +273,11 @@ DEV void sys_steps(int64_t (&acc)[8], const int32_t (&rc)[32], int32_t (&v)[8], 
             if (PM == PM_WIDE) pred = (int32_t)__builtin_amdgcn_alignbit(hi, lo, sh);
             else if (PM == PM_NARROW) pred = (int32_t)lo >> sh;
             else pred = (int32_t)__builtin_amdgcn_alignbit(wide ? hi : (uint32_t)((int32_t)lo >> 31), lo, sh);
-            if (FIRST && (uint32_t)t < order) pred = 0;
+            if (FIRST) {
+                uint32_t ord = order;
+                asm volatile("" : "+v"(ord)); /* compare per step: 32 hoisted lane masks spill */
+                pred = (uint32_t)t < ord ? 0 : pred;
+            }
             v[q] = (int32_t)((uint32_t)v[q] + (uint32_t)pred);
             acc[a] = 0;
         }
@@ -144,11 +288,10 @@ DEV void sys_steps(int64_t (&acc)[8], const int32_t (&rc)[32], int32_t (&v)[8], 
         case 2: bc = quad_bcast<2>(v[q]); break;
         default: bc = quad_bcast<3>(v[q]); break;
         }
+        int32_t cs[8];
 #pragma unroll
-        for (int a2 = 0; a2 < A; a2++) {
-            const int u = ((4 * a2 - t - 1) % P + P) % P;
-            acc[a2] = sys_mad(rc[u], bc, acc[a2]);
-        }
+        for (int a2 = 0; a2 < 8; a2++) cs[a2] = a2 < A ? rc[((4 * a2 - t - 1) % P + P) % P] : 0;
+        sys_macs<A>(acc, cs, bc);
     }
 }
 
@@ -193,10 +336,147 @@ DEV void sys_pack(const SysShared &S, const int32_t *row, uint32_t w, uint32_t l
     }
 }
 
+/* Fast pack: every frame of the wave has a full chunk, a power-of-two channel count and a
+ * 16-byte aligned run; each lane writes whole 16-byte pieces of the wave's runs (one store
+ * instruction covers the runs of several frames, coalesced).  Pieces per frame np: FLACDecoder
+ * stereo 8 (4 samples, L | R << 16), FLACDecoder other 4 (8 samples of channel 0, 16-bit),
+ * interleaved int32 8C (4 values), FLACFileReader 2C fb (16 bytes of fb-byte values), planar
+ * int32 8C (4 samples of one channel).  Returns false (nothing written) when the wave does not
+ * qualify. */
+DEV int32_t sys_val(const int32_t *row, uint32_t n, uint32_t s0, uint32_t c, uint32_t C, uint32_t as) {
+    if (C == 2u) {
+        const int2 x = *(const int2 *)(row + n * SYS_RP + s0);
+        int32_t l = x.x, r = x.y;
+        decorrelate(as, l, r);
+        return c ? r : l;
+    }
+    return row[n * SYS_RP + s0 + c];
+}
+DEV bool sys_pack_fast(const SysShared &S, const int32_t *row, uint32_t w, uint32_t lane, uint32_t lg, uint32_t n0, int fmt,
+                       const bnf_stream_params &sp, uint8_t *__restrict__ out) {
+    const uint32_t cl = 1u << lg, nfw = 16u >> lg, fl0 = (16u * w) >> lg;
+    const uint32_t fb = sp.bps == 24 ? 3u : 2u;
+    /* eligibility: every decoding frame of the wave (the channel count is the same for all
+     * frames of a stream here: anything else takes the generic pack) */
+    uint32_t C = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < nfw && ok; i++) {
+        const uint32_t fl = fl0 + i;
+        if (S.f_state[fl] != FS_DEC) continue;
+        const uint32_t c = S.f_ch[fl], bs = S.f_bs[fl];
+        const uint64_t os = S.f_os[fl];
+        if (C == 0u) C = c;
+        ok = c == C && (c & (c - 1u)) == 0u && n0 + SYS_CHK <= bs;
+        uint64_t base;
+        switch (fmt) {
+        case BNF_OUT_FLACDECODER: base = (os + n0) * (c == 2u ? 4u : 2u); break;
+        case BNF_OUT_INTERLEAVED32: ok = ok && c == sp.channels; base = (os + n0) * sp.channels * 4u; break;
+        case BNF_OUT_PLANAR32: ok = ok && (bs & 3u) == 0u; base = (os * sp.channels + n0) * 4u; break;
+        default: ok = ok && c == sp.channels; base = (os + n0) * sp.channels * fb; break;
+        }
+        ok = ok && (base & 15u) == 0u;
+    }
+    if (!ok) return false;
+    if (C == 0u) return true; /* nothing to write */
+    const uint32_t lc = __builtin_ctz(C);
+    uint32_t np, m3 = 0; /* np = pieces per frame; m3: np = 3 << e */
+    switch (fmt) {
+    case BNF_OUT_FLACDECODER: np = C == 2u ? 8u : 4u; break;
+    case BNF_OUT_INTERLEAVED32: case BNF_OUT_PLANAR32: np = 8u * C; break;
+    default: np = 2u * C * fb; m3 = fb == 3u; break;
+    }
+    const uint32_t e = m3 ? __builtin_ctz(np / 3u) : __builtin_ctz(np);
+    for (uint32_t P = lane; P < nfw * np; P += 64u) {
+        const uint32_t x = P >> e;
+        const uint32_t i = m3 ? (__umulhi(x, 0xAAAAAAABu) >> 1) : x; /* P / np */
+        const uint32_t p = P - i * np;
+        const uint32_t fl = fl0 + i;
+        if (S.f_state[fl] != FS_DEC) continue;
+        const uint32_t s0 = fl * cl, as = S.f_as[fl], bs = S.f_bs[fl];
+        const uint64_t os = S.f_os[fl];
+        u32x4 v;
+        uint64_t at;
+        switch (fmt) {
+        case BNF_OUT_FLACDECODER:
+            if (C == 2u) { /* FLACDecoder.cs:549-562: L | R << 16 */
+                uint32_t d[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int2 xx = *(const int2 *)(row + (4u * p + q) * SYS_RP + s0);
+                    int32_t l = xx.x, r = xx.y;
+                    decorrelate(as, l, r);
+                    d[q] = ((uint32_t)l & 0xffffu) | ((uint32_t)r << 16);
+                }
+                v = u32x4{d[0], d[1], d[2], d[3]};
+                at = (os + n0) * 4u + 16u * p;
+            } else { /* :564-577: channel 0 only, 16-bit */
+                uint32_t d[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    d[q] = ((uint32_t)row[(8u * p + 2u * q) * SYS_RP + s0] & 0xffffu) |
+                           ((uint32_t)row[(8u * p + 2u * q + 1u) * SYS_RP + s0] << 16);
+                v = u32x4{d[0], d[1], d[2], d[3]};
+                at = (os + n0) * 2u + 16u * p;
+            }
+            break;
+        case BNF_OUT_INTERLEAVED32: {
+            uint32_t d[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t vv = 4u * p + q;
+                d[q] = (uint32_t)sys_val(row, vv >> lc, s0, vv & (C - 1u), C, as);
+            }
+            v = u32x4{d[0], d[1], d[2], d[3]};
+            at = (os + n0) * sp.channels * 4u + 16u * p;
+            break;
+        }
+        case BNF_OUT_PLANAR32: {
+            const uint32_t c = p >> 3, pp = p & 7u;
+            uint32_t d[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) d[q] = (uint32_t)sys_val(row, 4u * pp + q, s0, c, C, as);
+            v = u32x4{d[0], d[1], d[2], d[3]};
+            at = (os * sp.channels + (uint64_t)c * bs + n0) * 4u + 16u * pp;
+            break;
+        }
+        default: /* FLACFileReader.cs:220-237: fb bytes per value, little-endian, sample-major */
+            if (fb == 3u) {
+                const uint32_t b0 = 16u * p, vlo = __umulhi(b0, 0xAAAAAAABu) >> 1, off = b0 - 3u * vlo;
+                int32_t xv[6];
+#pragma unroll
+                for (int q = 0; q < 6; q++) {
+                    const uint32_t vv = min(vlo + q, SYS_CHK * C - 1u);
+                    xv[q] = sys_val(row, vv >> lc, s0, vv & (C - 1u), C, as);
+                }
+                const uint32_t d0 = ((uint32_t)xv[0] & 0xFFFFFFu) | ((uint32_t)xv[1] << 24);
+                const uint32_t d1 = (((uint32_t)xv[1] >> 8) & 0xFFFFu) | ((uint32_t)xv[2] << 16);
+                const uint32_t d2 = (((uint32_t)xv[2] >> 16) & 0xFFu) | ((uint32_t)xv[3] << 8);
+                const uint32_t d3 = ((uint32_t)xv[4] & 0xFFFFFFu) | ((uint32_t)xv[5] << 24);
+                const uint32_t d4 = ((uint32_t)xv[5] >> 8) & 0xFFFFu;
+                v = u32x4{__builtin_amdgcn_alignbyte(d1, d0, off), __builtin_amdgcn_alignbyte(d2, d1, off),
+                          __builtin_amdgcn_alignbyte(d3, d2, off), __builtin_amdgcn_alignbyte(d4, d3, off)};
+            } else {
+                uint32_t d[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t v0 = 8u * p + 2u * q, v1 = v0 + 1u;
+                    d[q] = ((uint32_t)sys_val(row, v0 >> lc, s0, v0 & (C - 1u), C, as) & 0xffffu) |
+                           ((uint32_t)sys_val(row, v1 >> lc, s0, v1 & (C - 1u), C, as) << 16);
+                }
+                v = u32x4{d[0], d[1], d[2], d[3]};
+            }
+            at = (os + n0) * sp.channels * fb + 16u * p;
+            break;
+        }
+        gst128((uint64_t)(uintptr_t)out + at, v);
+    }
+    return true;
+}
+
 /* ------------------------------------------------------------------ restore waves */
 template <int A, int PM>
 DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint32_t nchunks, int fmt,
-                     const bnf_stream_params &sp, uint8_t *__restrict__ out) {
+                     const bnf_stream_params &sp, uint8_t *__restrict__ out, uint32_t ablate) {
     constexpr int P = 4 * A;
     const uint32_t g = lane >> 2, j = lane & 3u, pl = 16u * w + g;
     const uint32_t order = S.p_order[pl], flags = S.p_flags[pl], wasted = S.p_wasted[pl], bs = S.p_bs[pl];
@@ -210,14 +490,18 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
 #pragma unroll
     for (int a = 0; a < 8; a++) acc[a] = 0;
     bool range_bad = false;
+    const bool tm = (ablate & 0x100u) != 0;
+    uint64_t t_st = 0, t_pk = 0, t_bw = 0;
     sys_bar(); /* end of iteration 0: the producer's chunk 0 is in rows[0]; rows[1] may be overwritten */
     for (uint32_t k = 1; k <= nchunks; k++) {
+        const uint64_t t0 = sys_now(tm);
         const uint32_t n0 = (k - 1u) * SYS_CHK;
         int32_t *row = S.rows[(k - 1u) & 1u];
         int32_t v[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) v[q] = row[(j + 4u * q) * SYS_RP + pl];
-        if (k == 1u) sys_steps<A, PM, true>(acc, rc, v, j, sh, wide, order);
+        if (ablate & 4u) { /* timing ablation: no restore */
+        } else if (k == 1u) sys_steps<A, PM, true>(acc, rc, v, j, sh, wide, order);
         else sys_steps<A, PM, false>(acc, rc, v, j, sh, wide, order);
 #pragma unroll
         for (int q = 0; q < 8; q++) {
@@ -228,18 +512,32 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
             }
         }
         lds_sync();
-        sys_pack(S, row, w, lane, lg, n0, fmt, sp, out);
+        const uint64_t t1 = sys_now(tm);
+        if (!(ablate & 2u)) {
+            if ((ablate & 0x400000u) || !sys_pack_fast(S, row, w, lane, lg, n0, fmt, sp, out))
+                sys_pack(S, row, w, lane, lg, n0, fmt, sp, out);
+        }
+        const uint64_t t2 = sys_now(tm);
         sys_bar();
+        const uint64_t t3 = sys_now(tm);
+        t_st += t1 - t0;
+        t_pk += t2 - t1;
+        t_bw += t3 - t2;
+    }
+    if (tm && lane == 0) {
+        atomicAdd(&g_stats[11], (unsigned long long)t_st);
+        atomicAdd(&g_stats[12], (unsigned long long)t_pk);
+        atomicAdd(&g_stats[13], (unsigned long long)t_bw);
     }
     if (range_bad) S.f_bad[pl >> lg] = 1u;
 }
 
 template <int A>
 DEV void sys_restore_pm(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint32_t nchunks, int fmt,
-                        const bnf_stream_params &sp, uint8_t *out, int pm) {
-    if (pm == PM_WIDE) sys_restore<A, PM_WIDE>(S, w, lane, lg, nchunks, fmt, sp, out);
-    else if (pm == PM_NARROW) sys_restore<A, PM_NARROW>(S, w, lane, lg, nchunks, fmt, sp, out);
-    else sys_restore<A, PM_MIXED>(S, w, lane, lg, nchunks, fmt, sp, out);
+                        const bnf_stream_params &sp, uint8_t *out, int pm, uint32_t ablate) {
+    if (pm == PM_WIDE) sys_restore<A, PM_WIDE>(S, w, lane, lg, nchunks, fmt, sp, out, ablate);
+    else if (pm == PM_NARROW) sys_restore<A, PM_NARROW>(S, w, lane, lg, nchunks, fmt, sp, out, ablate);
+    else sys_restore<A, PM_MIXED>(S, w, lane, lg, nchunks, fmt, sp, out, ablate);
 }
 
 /* ------------------------------------------------------------------ the kernel */
@@ -308,6 +606,8 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         /* ---- subframe header: warm-ups into rows[0], coefficients into the table (rows[1]) */
         BR b;
         br_init(b, words, nbytes, (lds_u32 *)S.ring, lane, SYS_RD);
+        b.stats = (ablate & 0x100u) != 0; /* debug event counters (bench.py --stats) */
+        STAT(b.stats, 5);
         RS rs;
         rs.verb = 0; rs.k = 0; rs.esc = 0; rs.left = 0; rs.pidx = 0; rs.nparts = 0; rs.psamples = 0;
         rs.order = 0; rs.plen = 4; rs.pesc = 15; rs.porder = 0;
@@ -383,27 +683,64 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         if (lane == 0) S.nchunks = nchunks;
         wait_vm(); /* setup loads and seeks done: the refill counts start from zero */
         SysQ q;
-        q.d_last = 0;
-        q.e1 = b.iend;
+        q.d0 = q.d1 = q.d2 = 0;
+        q.e0 = q.e1 = q.e2 = b.iend;
         sys_bar(); /* B0: tables ready */
         /* ================================================= producer: chunks */
+        const bool tm = b.stats;
+        uint64_t t_ref = 0, t_dec = 0, t_bar = 0;
         for (uint32_t k = 0; k <= nchunks; k++) {
             if (k < nchunks) {
                 const uint32_t n0 = k * SYS_CHK;
                 int32_t *row = S.rows[k & 1u] + lane;
 #pragma unroll
-                for (uint32_t hh = 0; hh < 2u; hh++) {
-                    const uint32_t h0 = n0 + 16u * hh;
-                    sys_refill(b, active && h0 < bs, q);
-                    const uint32_t lo = max(h0, order), hi = active ? min(h0 + 16u, bs) : 0u;
-                    if (ablate & 8u) {
-                        for (uint32_t n = lo; n < hi; n++) row[(n - n0) * SYS_RP] = 0;
-                    } else {
-                        for (uint32_t n = lo; n < hi; n++) row[(n - n0) * SYS_RP] = rice_fused(b, rs, limit, trunc, nullptr);
+                for (uint32_t hh = 0; hh < SYS_CHK / SYS_HALF; hh++) {
+                    const uint32_t h0 = n0 + SYS_HALF * hh;
+                    STAT(b.stats && active && h0 < bs, 4);
+                    const uint64_t t0 = sys_now(tm);
+                    if (!(ablate & 0x80000u)) sys_refill(b, active && h0 < bs, q); /* ablation: landings only */
+                    const uint64_t t1 = sys_now(tm);
+                    /* a run of SYS_HALF codewords of one Rice partition on every lane still decoding
+                     * (partitions of 16 or more samples start on a run: their sizes are powers of
+                     * two, partition 0 ends at one); else residual by residual */
+                    const bool run = active && h0 + SYS_HALF <= bs && h0 >= order;
+                    if (any_lane(run && rs.left == 0u && rs.pidx < rs.nparts)) {
+                        if (run && rs.left == 0u && rs.pidx < rs.nparts) read_partition(b, rs);
                     }
+                    const bool fast = !(ablate & 0x200000u) && !any_lane(active && h0 < bs && !(run && !rs.esc && rs.left >= SYS_HALF));
+                    if (fast && any_lane(run)) {
+                        int32_t r[SYS_HALF];
+                        const uint32_t kk = run ? rs.k : 0u;
+                        uint32_t kmax = kk;
+                        for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor(kmax, o));
+                        if (kmax <= 9u) sys_rice_run<true>(b, run, kk, 31u - kk, kk + 1u, 32u - kk, r, limit, trunc, lane);
+                        else sys_rice_run<false>(b, run, kk, 31u - kk, kk + 1u, 32u - kk, r, limit, trunc, lane);
+                        if (run) {
+                            rs.left -= SYS_HALF;
+#pragma unroll
+                            for (int i = 0; i < SYS_HALF; i++) row[(h0 - n0 + (uint32_t)i) * SYS_RP] = r[i];
+                        }
+                    } else {
+                        const uint32_t lo = max(h0, order), hi = active ? min(h0 + SYS_HALF, bs) : 0u;
+                        if (ablate & 8u) {
+                            for (uint32_t n = lo; n < hi; n++) row[(n - n0) * SYS_RP] = 0;
+                        } else {
+                            for (uint32_t n = lo; n < hi; n++) row[(n - n0) * SYS_RP] = rice_fused(b, rs, limit, trunc, nullptr);
+                        }
+                    }
+                    const uint64_t t2 = sys_now(tm);
+                    t_ref += t1 - t0;
+                    t_dec += t2 - t1;
                 }
             }
+            const uint64_t t3 = sys_now(tm);
             sys_bar();
+            t_bar += sys_now(tm) - t3;
+        }
+        if (tm && lane == 0) {
+            atomicAdd(&g_stats[8], (unsigned long long)t_ref);
+            atomicAdd(&g_stats[9], (unsigned long long)t_dec);
+            atomicAdd(&g_stats[10], (unsigned long long)t_bar);
         }
         /* ================================================= producer: tail (read_frame_ @0x100118c0) */
         const bool last = active && ch + 1u == fi.channels;
@@ -453,10 +790,10 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         for (int o = 32; o > 0; o >>= 1) ord = max(ord, (uint32_t)__shfl_xor(ord, o));
         const bool any_w = any_lane(act && (fl & SF_WIDE)), any_n = any_lane(act && !(fl & SF_WIDE));
         const int pm = (ablate & 0x40000u) ? PM_MIXED : any_w ? (any_n ? PM_MIXED : PM_WIDE) : PM_NARROW;
-        if (ord <= 4u) sys_restore_pm<1>(S, w, lane, lg, nchunks, fmt, sp, out, pm);
-        else if (ord <= 8u) sys_restore_pm<2>(S, w, lane, lg, nchunks, fmt, sp, out, pm);
-        else if (ord <= 16u) sys_restore_pm<4>(S, w, lane, lg, nchunks, fmt, sp, out, pm);
-        else sys_restore_pm<8>(S, w, lane, lg, nchunks, fmt, sp, out, pm);
+        if (ord <= 4u) sys_restore_pm<1>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate);
+        else if (ord <= 8u) sys_restore_pm<2>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate);
+        else if (ord <= 16u) sys_restore_pm<4>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate);
+        else sys_restore_pm<8>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate);
     }
     sys_bar(); /* tail done: frame table complete, CRC tables in rows[0] */
     /* ---- CRC-16 check, records, zero fill, hand-back (this wave's frames) */
@@ -526,6 +863,17 @@ hipError_t bnf_upload_tables_tu8(const uint8_t *crc8, const uint16_t *crc16x8, c
     return upload_tables(crc8, crc16x8, xpow);
 }
 void bnf_set_ablate_tu8(uint32_t v) { g_ablate = v; }
+hipError_t bnf_stats_tu8(uint64_t *out16, int reset) {
+    uint64_t v[16];
+    hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < 16; i++) out16[i] += v[i];
+    if (reset) {
+        static const uint64_t z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z);
+    }
+    return e;
+}
 /* redo: [0] hand-back count (zeroed by the caller), [4..] the frames handed back */
 hipError_t bnf_launch_decode_sys_tu8(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                      uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,

@@ -67,3 +67,43 @@ def gather_bytes(local, group=None, dst: int = 0):
         for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), glob(dst), group)]):
             req.wait()
     return None
+
+
+def gather_sizes(local, group=None):
+    """Every rank's byte count (one all_gather of an int64), for gather_post."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    return [int(x.item()) for x in sizes]
+
+
+def gather_post(local, sizes, group=None, dst: int = 0, parts=None):
+    """Post one gather of `local` to `dst` (sizes from gather_sizes) without waiting: returns
+    (works, parts).  On `dst`, parts are the receive buffers in rank order (pass the previous
+    call's to reuse them; parts[dst] is `local` itself); elsewhere None.  Under RCCL the ops
+    run on the communicator's stream, ordered after the work already enqueued on the current
+    stream (the decode of `local`) and concurrent with work enqueued after them (the next
+    step's decode into another buffer): bench.py's C5 flow overlaps step s's gather with step
+    s + 1's decode this way.  work.wait() orders the current stream after the transfer."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
+    if rank == dst:
+        if parts is None:
+            parts = [None] * world
+            for r in range(world):
+                if r != rank:
+                    parts[r] = torch.empty(sizes[r], dtype=local.dtype, device=local.device)
+        parts[rank] = local
+        ops = [dist.P2POp(dist.irecv, parts[r], glob(r), group) for r in range(world) if r != rank and sizes[r]]
+        return (dist.batch_isend_irecv(ops) if ops else []), parts
+    if local.numel():
+        return dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), glob(dst), group)]), None
+    return [], None

@@ -117,3 +117,53 @@ def test_concurrent_gather_three_ranks_ragged():
         pr.join(timeout=60)
         assert pr.exitcode == 0
     assert got == bytes([1] * 5 + [3] * 70001)
+
+
+def _pipeline_worker(rank, world, port, steps, result_q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 1000 + 37 * rank  # unequal shards
+        bufs = [torch.zeros(n, dtype=torch.uint8), torch.zeros(n, dtype=torch.uint8)]
+        sizes = shard.gather_sizes(bufs[0])
+        pend, parts = [[], []], [None, None]
+        for st in range(steps):
+            b = st % 2
+            for w in pend[b]:
+                w.wait()
+            bufs[b].copy_(torch.arange(n, dtype=torch.int64).add(rank * 7 + st * 13).remainder(251).to(torch.uint8))
+            pend[b], parts[b] = shard.gather_post(bufs[b], sizes, parts=parts[b])
+        for b in (0, 1):
+            for w in pend[b]:
+                w.wait()
+        if rank == 0:
+            result_q.put(torch.cat(parts[(steps - 1) % 2]).numpy().tobytes())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_overlapped_gather_pipeline(world):
+    """bench.py's overlapped C5 flow: two output buffers, step s's gather posted
+    (shard.gather_post) while step s + 1 fills the other buffer; rank 0 ends with the last
+    step's bytes of every rank, in rank order."""
+    import torch
+    import torch.multiprocessing as mp
+    steps = 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=120)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    st = steps - 1
+    ref = b"".join(torch.arange(1000 + 37 * r, dtype=torch.int64).add(r * 7 + st * 13).remainder(251).to(torch.uint8)
+                   .numpy().tobytes() for r in range(world))
+    assert got == ref

@@ -1,10 +1,30 @@
 #!/bin/bash
-# A/B timing of one library under environment settings: usage AB_VAR=NAME tools/ab_env.sh v1 v2 ...
+# A/B of environment settings on the bench's headline configs (one gpurun call, one box):
+#   ENVS="BNFLAC_DECODE_SYS=0;BNFLAC_DECODE_SYS=1" CFGS="C2 C3 C4 C5" ROUNDS=2 TAG=ab bash tools/ab_env.sh
+# Each (round, env, cfg) runs bench.py without legs / baselines and prints the decode launch,
+# k_parse and step times; the JSON lines go to gpurun_out/${TAG}_<cfg>_<i>_<round>.json.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-for r in $(seq 1 ${AB_ROUNDS:-2}); do
-  for v in "$@"; do
-    env ${AB_VAR}=$v timeout -k 10 200 python bench.py --steps ${AB_STEPS:-10} --warmup 2 --no-cpu-baseline --no-pcie --no-index --no-reader --legs= ${AB_ARGS:-} > "gpurun_out/abenv_${AB_VAR}_${v}_$r.json" 2>/dev/null || { echo "bench $v failed"; exit 1; }
-    python3 -c "import json;d=json.loads(open('gpurun_out/abenv_${AB_VAR}_${v}_$r.json').read().strip().splitlines()[-1]);r=d['roofline'];print('${AB_VAR}=$v', 'round $r', 'value', d['value'], 'k_decode_ms', r['avg_launch_ms'], 'k_parse_ms', r['k_parse_avg_ms'], 'bitexact', d['bitexact'])"
+mkdir -p gpurun_out
+TAG=${TAG:-ab}
+IFS=';' read -ra EV <<< "${ENVS:-BNFLAC_DECODE_SYS=0;BNFLAC_DECODE_SYS=1}"
+for r in $(seq 1 ${ROUNDS:-1}); do
+  for c in ${CFGS:-C2 C3 C4 C5}; do
+    x=""; [ $c = C5 ] && x="--c5-batch"
+    i=0
+    for e in "${EV[@]}"; do
+      out=gpurun_out/${TAG}_${c}_${i}_${r}.json
+      env $e timeout -k 10 ${BENCH_TIMEOUT:-240} python3 bench.py --config $c $x --steps ${STEPS:-5} --warmup 2 --legs= \
+          --no-cpu-baseline --no-pcie --no-index --no-reader ${EXTRA:-} --out $out > $out.log 2>&1
+      rc=$?
+      [ $rc -eq 0 ] || { echo "$c [$e] rc=$rc"; tail -5 $out.log; exit $rc; }
+      python3 - "$out" "$c" "$e" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1])); r = d["roofline"]
+print(f"{sys.argv[2]} [{sys.argv[3]}] {d['value']:.1f} MS/s step {d['ms_per_step']:.3f} ms decode {r['avg_launch_ms']:.3f} ms "
+      f"parse {r['k_parse_avg_ms']:.3f} ms frac {r['frac']:.3f} step_frac {r['step_frac']:.3f} bitexact {d['bitexact']}")
+PY
+      i=$((i + 1))
+    done
   done
 done
