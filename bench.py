@@ -776,7 +776,7 @@ def main():
         # k_decode_sys (BNFLAC_DECODE_SYS=1): s_memtime per producer wave / per restore wave
         line["stats"]["sys_cycles"] = {n: int(buf[8 + i]) // w for i, n in
                                        enumerate(["prod_refill", "prod_rice", "prod_barrier", "rest_steps",
-                                                  "rest_pack", "rest_barrier"])}
+                                                  "rest_pack", "rest_barrier", "refill_wait", "dma_in_flight"])}
     if args.ablate and rank == 0:
         abl = []
         for m in [int(x, 0) for x in args.ablate.split(",")]:

@@ -4262,13 +4262,16 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
 /* The library is built from this file three times (BNF_TU 0: sync scan + k_parse + shared
  * launchers, 1: k_decode<8>, 2: k_decode<32>), so the instances compile in parallel.  Each
  * TU is its own code object: the __constant__ tables are uploaded into every one. */
-static uint32_t g_ablate = 0xFFFFFFFFu;
+/* mode switches are read by launching threads while a test or tool may set them: atomics */
+static std::atomic<uint32_t> g_ablate{0xFFFFFFFFu};
 static uint32_t ablate_flags() {
-    if (g_ablate == 0xFFFFFFFFu) {
+    uint32_t v = g_ablate.load(std::memory_order_relaxed);
+    if (v == 0xFFFFFFFFu) {
         const char *e = getenv("BNFLAC_ABLATE"); /* timing experiments only: results are wrong */
-        g_ablate = e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+        v = e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+        g_ablate.store(v, std::memory_order_relaxed);
     }
-    return g_ablate;
+    return v;
 }
 static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc8_tab), crc8, 256);
@@ -4302,7 +4305,7 @@ extern "C" {
 hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     return upload_tables(crc8, crc16x8, xpow);
 }
-void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate = v; }
+void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate.store(v, std::memory_order_relaxed); }
 hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
     uint64_t v[16];
     hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
@@ -4346,7 +4349,7 @@ extern "C" {
 hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     return upload_tables(crc8, crc16x8, xpow);
 }
-void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate = v; }
+void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate.store(v, std::memory_order_relaxed); }
 hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
     uint64_t v[16];
     hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
@@ -4391,7 +4394,7 @@ extern "C" {
 hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     return upload_tables(crc8, crc16x8, xpow);
 }
-void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate = v; }
+void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate.store(v, std::memory_order_relaxed); }
 hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
     uint64_t v[16];
     hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
@@ -4787,14 +4790,21 @@ size_t bnf_decode_wave_lds(uint32_t cmax, uint32_t bsmax) { return (size_t)cmax 
 hipError_t TU_FN(bnf_launch_decode_wave)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                          int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info, uint32_t cmax,
                                          uint32_t bsmax, hipStream_t s) {
-    static const hipError_t attr = hipFuncSetAttribute((const void *)k_decode_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (160 << 10) - (int)(14u << 10)); /* rows above 64 KB */
-    if (attr != hipSuccess) return attr;
+    /* the dynamic-LDS limit is a per-device function attribute: set once for each device */
+    static std::atomic<uint8_t> attr_set[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (!attr_set[dev].load(std::memory_order_acquire)) {
+        const hipError_t attr = hipFuncSetAttribute((const void *)k_decode_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (160 << 10) - (int)(14u << 10)); /* rows above 64 KB */
+        if (attr != hipSuccess) return attr;
+        attr_set[dev].store(1, std::memory_order_release);
+    }
     hipLaunchKernelGGL(k_decode_wave, dim3(nframes), dim3(64), bnf_decode_wave_lds(cmax, bsmax), s, words, nbytes, nframes,
                        sp, fmt, out, out_bytes, info, cmax, bsmax, ablate_flags());
     return hipGetLastError();
 }
-void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate = v; }
+void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate.store(v, std::memory_order_relaxed); }
 hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
     uint64_t v[16];
     hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
@@ -4885,7 +4895,7 @@ uint32_t bnf_scan_blocks(uint64_t n) {
 }
 
 void bnf_set_ablate(uint32_t v) {
-    g_ablate = v;
+    g_ablate.store(v, std::memory_order_relaxed);
     bnf_set_ablate_tu1(v);
     bnf_set_ablate_tu2(v);
     bnf_set_ablate_tu3(v);
@@ -5053,13 +5063,15 @@ static SideQ *side_queue() { /* under g_side_mu; nullptr: decode serially */
  * 0.32, 3,752 3.33 vs 0.53; C4 4,096 2.56 vs 1.69.  The lane walk only wins once there are
  * ~256 lane-waves of short-partition frames: wave up to 8,192 frames, and up to 32,768 for
  * streams whose subframes are long (above 16 bits or more than 2 channels). */
-static int g_parse_wave = -1;
+static std::atomic<int> g_parse_wave{-1};
 static bool use_parse_wave(uint32_t nframes, const bnf_stream_params &sp) {
-    if (g_parse_wave < 0) {
+    int m = g_parse_wave.load(std::memory_order_relaxed);
+    if (m < 0) {
         const char *e = getenv("BNFLAC_PARSE_WAVE");
-        g_parse_wave = e ? (atoi(e) ? 1 : 0) : 2;
+        m = e ? (atoi(e) ? 1 : 0) : 2;
+        g_parse_wave.store(m, std::memory_order_relaxed);
     }
-    if (g_parse_wave != 2) return g_parse_wave == 1;
+    if (m != 2) return m == 1;
     return nframes <= 8192u || (nframes <= 32768u && (sp.bps > 16u || sp.channels > 2u));
 }
 
@@ -5070,16 +5082,18 @@ static bool use_parse_wave(uint32_t nframes, const bnf_stream_params &sp) {
 #ifndef DW_AUTO
 #define DW_AUTO 0 /* auto mode off until k_decode_wave beats the lane kernels on small batches */
 #endif
-static int g_decode_wave = -1;
+static std::atomic<int> g_decode_wave{-1};
 static bool use_decode_wave(uint32_t nframes, uint32_t cmax, uint32_t bsmax) {
-    if (g_decode_wave < 0) {
+    int m = g_decode_wave.load(std::memory_order_relaxed);
+    if (m < 0) {
         const char *e = getenv("BNFLAC_DECODE_WAVE");
-        g_decode_wave = e ? (atoi(e) ? 1 : 0) : 2;
+        m = e ? (atoi(e) ? 1 : 0) : 2;
+        g_decode_wave.store(m, std::memory_order_relaxed);
     }
-    if (!g_decode_wave || !bsmax || !cmax || cmax > 8u) return false;
+    if (!m || !bsmax || !cmax || cmax > 8u) return false;
     const size_t lds = bnf_decode_wave_lds(cmax, bsmax), fixed = 14u << 10;
     if (lds + fixed > (160u << 10)) return false;
-    if (g_decode_wave == 1) return true;
+    if (m == 1) return true;
     static const uint32_t cus = [] {
         int d = 0, cu = 256;
         if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
@@ -5108,8 +5122,8 @@ static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32
 
 extern "C" {
 void bnf_set_decode_sys(int mode) { g_decode_sys.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
-void bnf_set_decode_wave(int mode) { g_decode_wave = mode < 0 ? 2 : (mode ? 1 : 0); } /* -1: auto */
-void bnf_set_parse_wave(int mode) { g_parse_wave = mode < 0 ? 2 : (mode ? 1 : 0); } /* -1: auto */
+void bnf_set_decode_wave(int mode) { g_decode_wave.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
+void bnf_set_parse_wave(int mode) { g_parse_wave.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
 hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset) { /* debug counters of k_parse_wave (BNFLAC_PW_STATS=1) */
     hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_pw_stats), 8 * sizeof(uint64_t));
     if (e == hipSuccess && reset) {

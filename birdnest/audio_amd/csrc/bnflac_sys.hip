@@ -95,8 +95,18 @@ struct SysQ {
     uint32_t d0, d1, d2;
     uint32_t e0, e1, e2;
 };
-DEV void sys_refill(BR &b, bool want, SysQ &q) {
+__device__ unsigned long long g_sys_dbg[4]; /* debug: refill wait cycles, DMA instructions (stats mode) */
+DEV void sys_refill(BR &b, bool want, SysQ &q, bool tm = false) {
+    const uint64_t tw = tm ? __builtin_amdgcn_s_memtime() : 0ull;
     wait_vm_n(q.d0 + q.d1 + q.d2);
+    if (tm) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t dt = __builtin_amdgcn_s_memtime() - tw;
+        if ((threadIdx.x & 63u) == 0u) {
+            atomicAdd(&g_sys_dbg[0], dt);
+            atomicAdd(&g_sys_dbg[1], (unsigned long long)(q.d0 + q.d1 + q.d2));
+        }
+    }
     b.vendw = max(b.vendw, q.e2 * 4u); /* issued before the refill three back: landed */
     q.e2 = q.e1;
     q.e1 = q.e0;
@@ -217,34 +227,42 @@ DEV int64_t sys_mad(int32_t c, int32_t x, int64_t acc) {
     asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=&v"(d), "=&s"(co) : "v"(c), "v"(x), "v"(acc));
     return d;
 }
-/* acc[a] += c[a] * bc for a < A, exactly (v_mad_i64_i32), as ONE asm statement: the compiler
- * puts a wait state after every inline asm statement it cannot see into */
-template <int A> DEV void sys_macs(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc);
-template <> DEV void sys_macs<1>(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
-    uint64_t co;
-    asm("v_mad_i64_i32 %0, %1, %3, %2, %0"
-        : "+v"(acc[0]), "=&s"(co)
-        : "v"(bc), "v"(c[0]));
-}
-template <> DEV void sys_macs<2>(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
-    uint64_t co;
-    asm("v_mad_i64_i32 %0, %2, %4, %3, %0\n\t"
+/* acc[(a + R) % A] += c[(a + R) % A] * bc for a < A, exactly (v_mad_i64_i32), as ONE asm
+ * statement (the compiler puts a wait state after every inline asm statement it cannot see
+ * into), in the order a = 0, 1, ...: slot R -- the one the next step finalises -- first */
+template <int A, int R> DEV void sys_macs(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc);
+template <int R> struct SysMacs1 {
+    static DEV void run(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+        uint64_t co;
+        asm("v_mad_i64_i32 %0, %1, %3, %2, %0"
+            : "+v"(acc[(0 + R) % 1]), "=&s"(co)
+            : "v"(bc), "v"(c[(0 + R) % 1]));
+    }
+};
+template <int R> struct SysMacs2 {
+    static DEV void run(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+        uint64_t co;
+        asm("v_mad_i64_i32 %0, %2, %4, %3, %0\n\t"
         "v_mad_i64_i32 %1, %2, %5, %3, %1"
-        : "+v"(acc[0]), "+v"(acc[1]), "=&s"(co)
-        : "v"(bc), "v"(c[0]), "v"(c[1]));
-}
-template <> DEV void sys_macs<4>(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
-    uint64_t co;
-    asm("v_mad_i64_i32 %0, %4, %6, %5, %0\n\t"
+            : "+v"(acc[(0 + R) % 2]), "+v"(acc[(1 + R) % 2]), "=&s"(co)
+            : "v"(bc), "v"(c[(0 + R) % 2]), "v"(c[(1 + R) % 2]));
+    }
+};
+template <int R> struct SysMacs4 {
+    static DEV void run(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+        uint64_t co;
+        asm("v_mad_i64_i32 %0, %4, %6, %5, %0\n\t"
         "v_mad_i64_i32 %1, %4, %7, %5, %1\n\t"
         "v_mad_i64_i32 %2, %4, %8, %5, %2\n\t"
         "v_mad_i64_i32 %3, %4, %9, %5, %3"
-        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "=&s"(co)
-        : "v"(bc), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]));
-}
-template <> DEV void sys_macs<8>(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
-    uint64_t co;
-    asm("v_mad_i64_i32 %0, %8, %10, %9, %0\n\t"
+            : "+v"(acc[(0 + R) % 4]), "+v"(acc[(1 + R) % 4]), "+v"(acc[(2 + R) % 4]), "+v"(acc[(3 + R) % 4]), "=&s"(co)
+            : "v"(bc), "v"(c[(0 + R) % 4]), "v"(c[(1 + R) % 4]), "v"(c[(2 + R) % 4]), "v"(c[(3 + R) % 4]));
+    }
+};
+template <int R> struct SysMacs8 {
+    static DEV void run(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+        uint64_t co;
+        asm("v_mad_i64_i32 %0, %8, %10, %9, %0\n\t"
         "v_mad_i64_i32 %1, %8, %11, %9, %1\n\t"
         "v_mad_i64_i32 %2, %8, %12, %9, %2\n\t"
         "v_mad_i64_i32 %3, %8, %13, %9, %3\n\t"
@@ -252,47 +270,62 @@ template <> DEV void sys_macs<8>(int64_t (&acc)[8], const int32_t (&c)[8], int32
         "v_mad_i64_i32 %5, %8, %15, %9, %5\n\t"
         "v_mad_i64_i32 %6, %8, %16, %9, %6\n\t"
         "v_mad_i64_i32 %7, %8, %17, %9, %7"
-        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7]), "=&s"(co)
-        : "v"(bc), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]));
+            : "+v"(acc[(0 + R) % 8]), "+v"(acc[(1 + R) % 8]), "+v"(acc[(2 + R) % 8]), "+v"(acc[(3 + R) % 8]), "+v"(acc[(4 + R) % 8]), "+v"(acc[(5 + R) % 8]), "+v"(acc[(6 + R) % 8]), "+v"(acc[(7 + R) % 8]), "=&s"(co)
+            : "v"(bc), "v"(c[(0 + R) % 8]), "v"(c[(1 + R) % 8]), "v"(c[(2 + R) % 8]), "v"(c[(3 + R) % 8]), "v"(c[(4 + R) % 8]), "v"(c[(5 + R) % 8]), "v"(c[(6 + R) % 8]), "v"(c[(7 + R) % 8]));
+    }
+};
+template <int A, int R> DEV void sys_macs(int64_t (&acc)[8], const int32_t (&c)[8], int32_t bc) {
+    if constexpr (A == 1) SysMacs1<R>::run(acc, c, bc);
+    else if constexpr (A == 2) SysMacs2<R>::run(acc, c, bc);
+    else if constexpr (A == 4) SysMacs4<R>::run(acc, c, bc);
+    else SysMacs8<R>::run(acc, c, bc);
 }
+
 /* lane j's broadcast of lane JJ of its quad (DPP quad_perm) */
 template <int JJ> DEV int32_t quad_bcast(int32_t x) { return __builtin_amdgcn_mov_dpp(x, JJ * 0x55, 0xF, 0xF, false); }
 
 /* 32 samples of a chunk.  v[q]: on entry the residual (or warm-up) of sample n0 + j + 4q, on exit
  * the sample.  FIRST: chunk 0, where samples below the order are raw warm-ups. */
+template <int A, int PM, bool FIRST, int T>
+DEV void sys_step(int64_t (&acc)[8], const int32_t (&rc)[32], int32_t (&v)[8], uint32_t j, uint32_t sh, bool wide,
+                  uint32_t order) {
+    constexpr int P = 4 * A, jj = T & 3, q = T >> 2, a = q % A, an = ((T + 1) >> 2) % A;
+    /* finalise sample n0 + T: computed on every lane, kept by the lane that owns it (selects,
+     * not an exec-masked branch: no SALU, no branch per step) */
+    const bool own = j == (uint32_t)jj;
+    const uint32_t lo = (uint32_t)acc[a], hi = (uint32_t)((uint64_t)acc[a] >> 32);
+    int32_t pred;
+    if (PM == PM_WIDE) pred = (int32_t)__builtin_amdgcn_alignbit(hi, lo, sh);
+    else if (PM == PM_NARROW) pred = (int32_t)lo >> sh;
+    else pred = (int32_t)__builtin_amdgcn_alignbit(wide ? hi : (uint32_t)((int32_t)lo >> 31), lo, sh);
+    if (FIRST) {
+        uint32_t ord = order;
+        asm volatile("" : "+v"(ord)); /* compare per step: 32 hoisted lane masks spill */
+        pred = (uint32_t)T < ord ? 0 : pred;
+    }
+    const int32_t nv = (int32_t)((uint32_t)v[q] + (uint32_t)pred);
+    v[q] = own ? nv : v[q];
+    acc[a] = own ? 0 : acc[a]; /* the slot now holds sample n0 + T + P */
+    const int32_t bc = quad_bcast<jj>(v[q]);
+    int32_t cs[8];
+#pragma unroll
+    for (int a2 = 0; a2 < 8; a2++) cs[a2] = a2 < A ? rc[((4 * a2 - T - 1) % P + P) % P] : 0;
+    sys_macs<A, an>(acc, cs, bc);
+}
+template <int A, int PM, bool FIRST, int T>
+DEV void sys_steps_from(int64_t (&acc)[8], const int32_t (&rc)[32], int32_t (&v)[8], uint32_t j, uint32_t sh, bool wide,
+                        uint32_t order) {
+    if constexpr (T < 32) {
+        sys_step<A, PM, FIRST, T>(acc, rc, v, j, sh, wide, order);
+        sys_steps_from<A, PM, FIRST, T + 1>(acc, rc, v, j, sh, wide, order);
+    }
+}
+/* 32 samples of a chunk.  v[q]: on entry the residual (or warm-up) of sample n0 + j + 4q, on exit
+ * the sample.  FIRST: chunk 0, where samples below the order are raw warm-ups. */
 template <int A, int PM, bool FIRST>
 DEV void sys_steps(int64_t (&acc)[8], const int32_t (&rc)[32], int32_t (&v)[8], uint32_t j, uint32_t sh, bool wide,
                    uint32_t order) {
-    constexpr int P = 4 * A;
-#pragma unroll
-    for (int t = 0; t < 32; t++) {
-        const int jj = t & 3, q = t >> 2, a = q % A;
-        if (j == (uint32_t)jj) { /* finalise sample n0 + t in the lane that owns it */
-            const uint32_t lo = (uint32_t)acc[a], hi = (uint32_t)((uint64_t)acc[a] >> 32);
-            int32_t pred;
-            if (PM == PM_WIDE) pred = (int32_t)__builtin_amdgcn_alignbit(hi, lo, sh);
-            else if (PM == PM_NARROW) pred = (int32_t)lo >> sh;
-            else pred = (int32_t)__builtin_amdgcn_alignbit(wide ? hi : (uint32_t)((int32_t)lo >> 31), lo, sh);
-            if (FIRST) {
-                uint32_t ord = order;
-                asm volatile("" : "+v"(ord)); /* compare per step: 32 hoisted lane masks spill */
-                pred = (uint32_t)t < ord ? 0 : pred;
-            }
-            v[q] = (int32_t)((uint32_t)v[q] + (uint32_t)pred);
-            acc[a] = 0;
-        }
-        int32_t bc;
-        switch (jj) {
-        case 0: bc = quad_bcast<0>(v[q]); break;
-        case 1: bc = quad_bcast<1>(v[q]); break;
-        case 2: bc = quad_bcast<2>(v[q]); break;
-        default: bc = quad_bcast<3>(v[q]); break;
-        }
-        int32_t cs[8];
-#pragma unroll
-        for (int a2 = 0; a2 < 8; a2++) cs[a2] = a2 < A ? rc[((4 * a2 - t - 1) % P + P) % P] : 0;
-        sys_macs<A>(acc, cs, bc);
-    }
+    sys_steps_from<A, PM, FIRST, 0>(acc, rc, v, j, sh, wide, order);
 }
 
 /* ------------------------------------------------------------------ pack */
@@ -336,13 +369,15 @@ DEV void sys_pack(const SysShared &S, const int32_t *row, uint32_t w, uint32_t l
     }
 }
 
-/* Fast pack: every frame of the wave has a full chunk, a power-of-two channel count and a
- * 16-byte aligned run; each lane writes whole 16-byte pieces of the wave's runs (one store
- * instruction covers the runs of several frames, coalesced).  Pieces per frame np: FLACDecoder
- * stereo 8 (4 samples, L | R << 16), FLACDecoder other 4 (8 samples of channel 0, 16-bit),
- * interleaved int32 8C (4 values), FLACFileReader 2C fb (16 bytes of fb-byte values), planar
- * int32 8C (4 samples of one channel).  Returns false (nothing written) when the wave does not
- * qualify. */
+/* Fast pack: every decoding frame of the wave has a power-of-two channel count and a 16-byte
+ * aligned run; each lane writes whole 16-byte pieces of the wave's runs (one store instruction
+ * covers the runs of several frames, coalesced).  Pieces per frame np: FLACDecoder stereo 8
+ * (4 samples, L | R << 16), FLACDecoder other 4 (8 samples of channel 0, 16-bit), interleaved
+ * int32 8C (4 values), FLACFileReader 2C fb (16 bytes of fb-byte values), planar int32 8C (4
+ * samples of one channel).  The piece of each lane (at most two per lane: np <= 64 per frame,
+ * 16 subframe slots per wave) and its frame's fields are set up once (sys_pack_prep); a chunk
+ * then costs the value reads, the packing and one store per piece.  A chunk in which some frame
+ * ends part-way takes the generic pack. */
 DEV int32_t sys_val(const int32_t *row, uint32_t n, uint32_t s0, uint32_t c, uint32_t C, uint32_t as) {
     if (C == 2u) {
         const int2 x = *(const int2 *)(row + n * SYS_RP + s0);
@@ -352,50 +387,84 @@ DEV int32_t sys_val(const int32_t *row, uint32_t n, uint32_t s0, uint32_t c, uin
     }
     return row[n * SYS_RP + s0 + c];
 }
-DEV bool sys_pack_fast(const SysShared &S, const int32_t *row, uint32_t w, uint32_t lane, uint32_t lg, uint32_t n0, int fmt,
-                       const bnf_stream_params &sp, uint8_t *__restrict__ out) {
+struct SysPk {
+    bool ok;                 /* the wave qualifies (wave-uniform) */
+    uint32_t C, lc, fb, cbytes;
+    bool pv[2];              /* this lane's piece r exists and its frame decodes */
+    uint32_t s0[2], as[2], p[2], bs[2];
+    uint64_t at[2];          /* output byte of the piece in chunk 0 */
+};
+DEV void sys_pack_prep(SysPk &k, const SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, int fmt,
+                       const bnf_stream_params &sp) {
     const uint32_t cl = 1u << lg, nfw = 16u >> lg, fl0 = (16u * w) >> lg;
-    const uint32_t fb = sp.bps == 24 ? 3u : 2u;
-    /* eligibility: every decoding frame of the wave (the channel count is the same for all
-     * frames of a stream here: anything else takes the generic pack) */
+    k.fb = sp.bps == 24 ? 3u : 2u;
     uint32_t C = 0;
     bool ok = true;
-    for (uint32_t i = 0; i < nfw && ok; i++) {
+    for (uint32_t i = 0; i < nfw; i++) {
         const uint32_t fl = fl0 + i;
         if (S.f_state[fl] != FS_DEC) continue;
         const uint32_t c = S.f_ch[fl], bs = S.f_bs[fl];
         const uint64_t os = S.f_os[fl];
         if (C == 0u) C = c;
-        ok = c == C && (c & (c - 1u)) == 0u && n0 + SYS_CHK <= bs;
+        ok = ok && c == C && (c & (c - 1u)) == 0u;
         uint64_t base;
         switch (fmt) {
-        case BNF_OUT_FLACDECODER: base = (os + n0) * (c == 2u ? 4u : 2u); break;
-        case BNF_OUT_INTERLEAVED32: ok = ok && c == sp.channels; base = (os + n0) * sp.channels * 4u; break;
-        case BNF_OUT_PLANAR32: ok = ok && (bs & 3u) == 0u; base = (os * sp.channels + n0) * 4u; break;
-        default: ok = ok && c == sp.channels; base = (os + n0) * sp.channels * fb; break;
+        case BNF_OUT_FLACDECODER: base = os * (c == 2u ? 4u : 2u); break;
+        case BNF_OUT_INTERLEAVED32: ok = ok && c == sp.channels; base = os * sp.channels * 4u; break;
+        case BNF_OUT_PLANAR32: ok = ok && (bs & 3u) == 0u; base = os * sp.channels * 4u; break;
+        default: ok = ok && c == sp.channels; base = os * sp.channels * k.fb; break;
         }
         ok = ok && (base & 15u) == 0u;
     }
-    if (!ok) return false;
-    if (C == 0u) return true; /* nothing to write */
-    const uint32_t lc = __builtin_ctz(C);
+    k.ok = ok && C != 0u;
+    k.pv[0] = k.pv[1] = false;
+    if (!k.ok) return;
+    k.C = C;
+    k.lc = __builtin_ctz(C);
     uint32_t np, m3 = 0; /* np = pieces per frame; m3: np = 3 << e */
     switch (fmt) {
-    case BNF_OUT_FLACDECODER: np = C == 2u ? 8u : 4u; break;
-    case BNF_OUT_INTERLEAVED32: case BNF_OUT_PLANAR32: np = 8u * C; break;
-    default: np = 2u * C * fb; m3 = fb == 3u; break;
+    case BNF_OUT_FLACDECODER: np = C == 2u ? 8u : 4u; k.cbytes = SYS_CHK * (C == 2u ? 4u : 2u); break;
+    case BNF_OUT_INTERLEAVED32: np = 8u * C; k.cbytes = SYS_CHK * 4u * sp.channels; break;
+    case BNF_OUT_PLANAR32: np = 8u * C; k.cbytes = SYS_CHK * 4u; break;
+    default: np = 2u * C * k.fb; m3 = k.fb == 3u; k.cbytes = SYS_CHK * sp.channels * k.fb; break;
     }
     const uint32_t e = m3 ? __builtin_ctz(np / 3u) : __builtin_ctz(np);
-    for (uint32_t P = lane; P < nfw * np; P += 64u) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint32_t P = lane + 64u * r;
         const uint32_t x = P >> e;
         const uint32_t i = m3 ? (__umulhi(x, 0xAAAAAAABu) >> 1) : x; /* P / np */
-        const uint32_t p = P - i * np;
-        const uint32_t fl = fl0 + i;
-        if (S.f_state[fl] != FS_DEC) continue;
-        const uint32_t s0 = fl * cl, as = S.f_as[fl], bs = S.f_bs[fl];
+        const uint32_t pp = P - i * np;
+        const uint32_t fl = fl0 + min(i, nfw - 1u);
+        k.pv[r] = i < nfw && S.f_state[fl] == FS_DEC;
+        k.s0[r] = fl * cl;
+        k.as[r] = S.f_as[fl];
+        k.bs[r] = S.f_bs[fl];
+        k.p[r] = pp;
         const uint64_t os = S.f_os[fl];
+        switch (fmt) {
+        case BNF_OUT_FLACDECODER: k.at[r] = os * (C == 2u ? 4u : 2u) + 16u * pp; break;
+        case BNF_OUT_INTERLEAVED32: k.at[r] = os * sp.channels * 4u + 16u * pp; break;
+        case BNF_OUT_PLANAR32: k.at[r] = (os * sp.channels + (uint64_t)(pp >> 3) * k.bs[r]) * 4u + 16u * (pp & 7u); break;
+        default: k.at[r] = os * sp.channels * k.fb + 16u * pp; break;
+        }
+    }
+}
+/* one chunk; false: the generic pack must run (a frame ends part-way through this chunk) */
+DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt, uint8_t *__restrict__ out) {
+    if (!k.ok) return false;
+    if (any_lane((k.pv[0] && n0 < k.bs[0] && n0 + SYS_CHK > k.bs[0]) || (k.pv[1] && n0 < k.bs[1] && n0 + SYS_CHK > k.bs[1])))
+        return false;
+    const uint32_t C = k.C, lc = k.lc;
+    const uint64_t cofs = (uint64_t)(n0 / SYS_CHK) * k.cbytes;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        if (!any_lane(k.pv[r])) break;
+        if (!k.pv[r] || n0 >= k.bs[r]) continue;
+        uint32_t s0 = k.s0[r], p = k.p[r];
+        const uint32_t as = k.as[r];
+        asm volatile("" : "+v"(s0), "+v"(p)); /* addresses per chunk: hoisted out of the chunk loop they take ~90 VGPRs */
         u32x4 v;
-        uint64_t at;
         switch (fmt) {
         case BNF_OUT_FLACDECODER:
             if (C == 2u) { /* FLACDecoder.cs:549-562: L | R << 16 */
@@ -403,12 +472,11 @@ DEV bool sys_pack_fast(const SysShared &S, const int32_t *row, uint32_t w, uint3
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int2 xx = *(const int2 *)(row + (4u * p + q) * SYS_RP + s0);
-                    int32_t l = xx.x, r = xx.y;
-                    decorrelate(as, l, r);
-                    d[q] = ((uint32_t)l & 0xffffu) | ((uint32_t)r << 16);
+                    int32_t l = xx.x, rr = xx.y;
+                    decorrelate(as, l, rr);
+                    d[q] = ((uint32_t)l & 0xffffu) | ((uint32_t)rr << 16);
                 }
                 v = u32x4{d[0], d[1], d[2], d[3]};
-                at = (os + n0) * 4u + 16u * p;
             } else { /* :564-577: channel 0 only, 16-bit */
                 uint32_t d[4];
 #pragma unroll
@@ -416,7 +484,6 @@ DEV bool sys_pack_fast(const SysShared &S, const int32_t *row, uint32_t w, uint3
                     d[q] = ((uint32_t)row[(8u * p + 2u * q) * SYS_RP + s0] & 0xffffu) |
                            ((uint32_t)row[(8u * p + 2u * q + 1u) * SYS_RP + s0] << 16);
                 v = u32x4{d[0], d[1], d[2], d[3]};
-                at = (os + n0) * 2u + 16u * p;
             }
             break;
         case BNF_OUT_INTERLEAVED32: {
@@ -427,7 +494,6 @@ DEV bool sys_pack_fast(const SysShared &S, const int32_t *row, uint32_t w, uint3
                 d[q] = (uint32_t)sys_val(row, vv >> lc, s0, vv & (C - 1u), C, as);
             }
             v = u32x4{d[0], d[1], d[2], d[3]};
-            at = (os + n0) * sp.channels * 4u + 16u * p;
             break;
         }
         case BNF_OUT_PLANAR32: {
@@ -436,11 +502,10 @@ DEV bool sys_pack_fast(const SysShared &S, const int32_t *row, uint32_t w, uint3
 #pragma unroll
             for (int q = 0; q < 4; q++) d[q] = (uint32_t)sys_val(row, 4u * pp + q, s0, c, C, as);
             v = u32x4{d[0], d[1], d[2], d[3]};
-            at = (os * sp.channels + (uint64_t)c * bs + n0) * 4u + 16u * pp;
             break;
         }
         default: /* FLACFileReader.cs:220-237: fb bytes per value, little-endian, sample-major */
-            if (fb == 3u) {
+            if (k.fb == 3u) {
                 const uint32_t b0 = 16u * p, vlo = __umulhi(b0, 0xAAAAAAABu) >> 1, off = b0 - 3u * vlo;
                 int32_t xv[6];
 #pragma unroll
@@ -465,10 +530,9 @@ DEV bool sys_pack_fast(const SysShared &S, const int32_t *row, uint32_t w, uint3
                 }
                 v = u32x4{d[0], d[1], d[2], d[3]};
             }
-            at = (os + n0) * sp.channels * fb + 16u * p;
             break;
         }
-        gst128((uint64_t)(uintptr_t)out + at, v);
+        gst128((uint64_t)(uintptr_t)out + k.at[r] + cofs, v);
     }
     return true;
 }
@@ -490,6 +554,8 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
 #pragma unroll
     for (int a = 0; a < 8; a++) acc[a] = 0;
     bool range_bad = false;
+    SysPk pk;
+    sys_pack_prep(pk, S, w, lane, lg, fmt, sp);
     const bool tm = (ablate & 0x100u) != 0;
     uint64_t t_st = 0, t_pk = 0, t_bw = 0;
     sys_bar(); /* end of iteration 0: the producer's chunk 0 is in rows[0]; rows[1] may be overwritten */
@@ -514,8 +580,7 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
         lds_sync();
         const uint64_t t1 = sys_now(tm);
         if (!(ablate & 2u)) {
-            if ((ablate & 0x400000u) || !sys_pack_fast(S, row, w, lane, lg, n0, fmt, sp, out))
-                sys_pack(S, row, w, lane, lg, n0, fmt, sp, out);
+            if ((ablate & 0x400000u) || !sys_pack_fast(pk, row, n0, fmt, out)) sys_pack(S, row, w, lane, lg, n0, fmt, sp, out);
         }
         const uint64_t t2 = sys_now(tm);
         sys_bar();
@@ -558,12 +623,24 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         const uint32_t slot = blockIdx.x * fpb + fl;
         const uint32_t f = (fl < fpb && slot < nframes) ? (perm ? perm[slot] : slot) : 0u;
         const bool have = fl < fpb && slot < nframes;
-        bnf_frame_info fi;
-        if (have) fi = info[f];
+        /* the record's fields one by one (a whole-record copy goes to scratch or, promoted, to LDS) */
+        struct { uint32_t status, flags, bps, channels, blocksize, assignment; uint64_t out_sample, frame_off; } fi;
+        fi.status = have ? info[f].status : (uint32_t)BNF_ST_SKIPPED;
+        fi.flags = fi.bps = fi.channels = fi.blocksize = fi.assignment = 0;
+        fi.out_sample = fi.frame_off = 0;
+        if (have) {
+            fi.flags = info[f].flags;
+            fi.bps = info[f].bps;
+            fi.channels = info[f].channels;
+            fi.blocksize = info[f].blocksize;
+            fi.assignment = info[f].assignment;
+            fi.out_sample = info[f].out_sample;
+            fi.frame_off = info[f].frame_off;
+        }
         const bool frame_ok = have && fi.status == BNF_ST_OK;
         if (ch == 0) { S.f_state[fl] = FS_NONE; S.f_bad[fl] = 0; }
         bool ok = false;
-        if (frame_ok && ch == 0) { /* decode_block's checks, with its records (SKIPPED) */
+        if (frame_ok && ch == 0) { /* decode_block's checks, with its records (SKIPPED: status and flags) */
             ok = true;
             uint32_t unsupported = 0;
             if (fmt == BNF_OUT_FLACDECODER && fi.bps != 16) unsupported = 1;          /* WriteCallback abort :526-530 */
@@ -571,9 +648,8 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             if (fmt == BNF_OUT_FILEREADER && sp.bps != 16 && sp.bps != 24) unsupported = 1; /* NotSupportedException :239-240 */
             if (unsupported) {
                 ok = false;
-                fi.status = BNF_ST_SKIPPED;
-                fi.flags |= 4u;
-                info[f] = fi;
+                info[f].status = BNF_ST_SKIPPED;
+                info[f].flags = fi.flags | 4u;
             } else {
                 uint64_t stride;
                 switch (fmt) {
@@ -583,13 +659,11 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                 }
                 if ((fi.out_sample + fi.blocksize) * stride > out_bytes) {
                     ok = false;
-                    fi.status = BNF_ST_SKIPPED;
-                    fi.flags |= 2u;
-                    info[f] = fi;
+                    info[f].status = BNF_ST_SKIPPED;
+                    info[f].flags = fi.flags | 2u;
                 } else if (fi.channels > chn_lanes) {
                     ok = false;
-                    fi.status = BNF_ST_SKIPPED;
-                    info[f] = fi;
+                    info[f].status = BNF_ST_SKIPPED;
                 }
             }
             S.f_idx[fl] = f;
@@ -624,7 +698,9 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             h.type = T_CONST; h.order = 0; h.wasted = 0; h.bps = 0; h.shift = 0; h.path = P_IA32; h.cval = 0;
             h.porder = 0; h.rice2 = 0;
             int32_t coef[32];
-            st = parse_subframe_head<true, 32, SYS_RP>(b, sub_bps(fi, ch), bs, limit, h, row0, coef, err);
+            /* subframe bps: +1 for the side channel (read_frame_ @0x100118c0, sub_bps) */
+            const uint32_t sbps = fi.bps + (((fi.assignment == 1u || fi.assignment == 3u) && ch == 1u) || (fi.assignment == 2u && ch == 0u) ? 1u : 0u);
+            st = parse_subframe_head<true, 32, SYS_RP>(b, sbps, bs, limit, h, row0, coef, err);
             if (st != BNF_ST_OK) {
                 bad = true;
             } else {
@@ -698,7 +774,7 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                     const uint32_t h0 = n0 + SYS_HALF * hh;
                     STAT(b.stats && active && h0 < bs, 4);
                     const uint64_t t0 = sys_now(tm);
-                    if (!(ablate & 0x80000u)) sys_refill(b, active && h0 < bs, q); /* ablation: landings only */
+                    if (!(ablate & 0x80000u)) sys_refill(b, active && h0 < bs, q, tm); /* ablation: landings only */
                     const uint64_t t1 = sys_now(tm);
                     /* a run of SYS_HALF codewords of one Rice partition on every lane still decoding
                      * (partitions of 16 or more samples start on a run: their sizes are powers of
@@ -862,10 +938,20 @@ extern "C" {
 hipError_t bnf_upload_tables_tu8(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
     return upload_tables(crc8, crc16x8, xpow);
 }
-void bnf_set_ablate_tu8(uint32_t v) { g_ablate = v; }
+void bnf_set_ablate_tu8(uint32_t v) { g_ablate.store(v, std::memory_order_relaxed); }
 hipError_t bnf_stats_tu8(uint64_t *out16, int reset) {
     uint64_t v[16];
     hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
+    if (e == hipSuccess) { /* slots 14, 15: refill wait cycles, DMA instructions waited past */
+        uint64_t d[4];
+        e = hipMemcpyFromSymbol(d, HIP_SYMBOL(g_sys_dbg), sizeof d);
+        v[14] += d[0];
+        v[15] += d[1];
+        if (e == hipSuccess && reset) {
+            static const uint64_t z4[4] = {0};
+            e = hipMemcpyToSymbol(HIP_SYMBOL(g_sys_dbg), z4, sizeof z4);
+        }
+    }
     if (e != hipSuccess) return e;
     for (int i = 0; i < 16; i++) out16[i] += v[i];
     if (reset) {
