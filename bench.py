@@ -6,12 +6,16 @@ stereo, blocksize 4096, LPC order 8, Rice partition order 4), compressed frames 
 HBM.  One step decodes ``--batches`` independent copies (distinct HBM regions, so nothing is
 served from a previous step's cache footprint) into FLACDecoder's 16-bit interleaved LE PCM
 (the OpenAL buffer-fill layout, FLACDecoder.cs:543-562) with the two launches of the path,
-k_parse and the decode launch (k_decode_st + k_decode<8|32>), on one HIP stream.
+k_parse and the decode launch, on one HIP stream.  The decode launch picks its kernels from the
+parse's frame classes: k_decode_st (stereo LPC <= 8, C2), k_decode_sw (24-bit stereo, C3),
+k_decode<8|16|32> (the rest), or k_decode_sys (the systolic LPC restore) for launches too small
+to fill the chip with one subframe per lane (C5, the reader).
 
 The other 1-GPU configs are side legs of the same line (rank 0, N = 1 only; `--legs`):
   C3  96 kHz/24-bit stereo, LPC-12, bs 8192, wasted bits + mid/side -> FLACFileReader 3-byte PCM
   C4  mixed CONSTANT/VERBATIM/FIXED/LPC, variable bs 192-16384, 16-bit stereo -> FLACDecoder PCM
-  C5  192 kHz/24-bit 8-channel LPC-32 files (469 frames each) -> FLACFileReader 3-byte PCM
+  C5  8 distinct 192 kHz/24-bit 8-channel LPC-32 files (469 frames each, c5_job at one rank)
+      -> FLACFileReader 3-byte PCM
 Each leg reports value, the decode launch's roofline, a step-level roofline and its own
 cpu_baseline.  `--config C5` makes C5 the headline: 8 files sharded over the ranks
 (shard.partition), each rank indexing its files on the GPU (bnflac_index_stream) and decoding
@@ -508,8 +512,24 @@ def reader_leg(wl, reps=3, chunk=16384):
 
 
 def leg(cfg, args, torch, dev, libflac, synth, dec, stream):
-    """One side config on this GPU: value, decode-launch roofline, step roofline, cpu_baseline."""
+    """One side config on this GPU: value, decode-launch roofline, step roofline, cpu_baseline.
+    C5: c5_job at one rank (the config's 8 distinct files in one launch pair), its cpu_baseline
+    on a sample of one of them."""
     c = CONFIGS[cfg]
+    if cfg == "C5":
+        r = c5_job(args, torch, None, dev, libflac, synth, dec, 1, 0, files=c["batches"], steps=args.leg_steps,
+                   warmup=1)
+        out = c5_summary(r, args, 1, steps=args.leg_steps)
+        for k in ("with_gather", "with_gather_overlapped", "ranks"):
+            out.pop(k, None)
+        out["steps"] = args.leg_steps
+        out["config"] = {"workload": c["desc"], "files": r["files"], "frames_per_step": r["frames_rank"]}
+        if not args.no_cpu_baseline:
+            wl = Workload(cfg, 1, 0, torch, dev, libflac, synth, dec)
+            out["cpu_baseline"] = cpu_leg(wl, args.leg_cpu_seconds, args.cpu_threads)
+            del wl
+        torch.cuda.empty_cache()
+        return out
     wl = Workload(cfg, c["batches"], 0, torch, dev, libflac, synth, dec)
     el, tp, td = timed(wl, args.leg_steps, 1, stream, 1, None, dev)
     ok = wl.check()
@@ -527,14 +547,16 @@ def leg(cfg, args, torch, dev, libflac, synth, dec, stream):
 
 
 # --------------------------------------------------------------------------- C5: files over ranks
-def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
+def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank, files=None, steps=None, warmup=None):
     """C5 as BASELINE.json states it: F files of 192 kHz/24-bit 8-channel LPC-32 audio sharded
     over the ranks (shard.partition by samples), each rank indexing its files on the GPU
     (bnflac_index_stream, untimed setup) and decoding them (timed: k_parse + decode launch over
     all its files at once), then the FLACFileReader PCM gathered to rank 0 (shard.gather_bytes:
     concurrent RCCL receives over xGMI)."""
     from birdnest.audio_amd import shard
-    F = args.batches or CONFIGS["C5"]["batches"]
+    F = files or args.batches or CONFIGS["C5"]["batches"]
+    steps = steps or steps
+    warmup = args.warmup if warmup is None else warmup
     p0 = synth.config("C5")
     ranges = shard.partition([p0.nframes * p0.blocksize] * F, world)  # equal files: F/world each
     lo, hi = ranges[rank]
@@ -564,33 +586,38 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
     stream = torch.cuda.current_stream(dev)
     nb = int(base[-1])
 
-    def decode(out=d_out):
+    def decode(out=d_out, e=None):
         if nframes:
             dec.parse_frames(d_bytes, nb, d_offs, nframes, sp, d_info, d_out_sample=d_os, stream=stream)
+            if e is not None:
+                e[1].record(stream)
             dec.decode_parsed(d_bytes, nb, nframes, sp, fmt, out, d_info, stream=stream)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         decode()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     ev = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    for _ in range(steps):
+        e = tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
         e[0].record(stream)
-        decode()
-        e[1].record(stream)
+        e[1].record(stream)  # re-recorded between the two launches when there are frames
+        decode(e=e)
+        e[2].record(stream)
         ev.append(e)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t_dec = time.perf_counter() - t0
-    t_launch = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    t_launch = sum(a.elapsed_time(c) for a, _, c in ev) / len(ev)
+    t_parse = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
+    t_decode = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
     # decode + gather: the same steps, each followed by the gather of every rank's PCM to rank 0
     gathered = None
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         decode()
         if world > 1:
             gathered = shard.gather_bytes(d_out[:nsmp * stride])
@@ -613,7 +640,7 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
         torch.cuda.synchronize(dev)
         dist.barrier()
         t0 = time.perf_counter()
-        for st in range(args.steps):
+        for st in range(steps):
             b = st % 2
             for wk in pend[b]:
                 wk.wait()
@@ -625,7 +652,7 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
         torch.cuda.synchronize(dev)
         dist.barrier()
         t_ovl = time.perf_counter() - t0
-        last = (args.steps - 1) % 2
+        last = (steps - 1) % 2
         if rank == 0 and parts[last] is not None:
             gathered_ovl = torch.cat(parts[last])
     if world > 1:
@@ -652,24 +679,27 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank):
     comp = sum(len(s.data) - int(s.frame_offsets[0]) for s in streams)
     alg = comp + nsmp * stride
     return {"samples": samples, "t_dec": t_dec, "t_all": t_all, "t_ovl": t_ovl, "t_launch": t_launch, "ok": ok,
+            "t_parse": t_parse, "t_decode": t_decode,
             "files": F, "alg_bytes_rank": alg, "frames_rank": nframes}
 
 
-def c5_summary(r, args, world):
-    """value / timing / roofline fields of a c5_job result (the --config C5 line, or the C5 flow
-    leg of a multi-GPU C2 run)."""
-    step_ms = r["t_dec"] / args.steps * 1e3
-    out = {"value": round(r["samples"] * args.steps / r["t_dec"] / 1e6, 2), "unit": "MSamples/s",
+def c5_summary(r, args, world, steps=None):
+    """value / timing / roofline fields of a c5_job result (the --config C5 line, the C5 leg at
+    N = 1, or the C5 flow leg of a multi-GPU C2 run)."""
+    steps = steps or steps
+    step_ms = r["t_dec"] / steps * 1e3
+    out = {"value": round(r["samples"] * steps / r["t_dec"] / 1e6, 2), "unit": "MSamples/s",
            "ms_per_step": round(step_ms, 4), "bitexact": r["ok"], "files": r["files"], "ranks": world,
-           "roofline": roofline(r["alg_bytes_rank"], r["t_launch"], 0.0, step_ms),
-           "with_gather": {"value": round(r["samples"] * args.steps / r["t_all"] / 1e6, 2), "unit": "MSamples/s",
-                           "ms_per_step": round(r["t_all"] / args.steps * 1e3, 4),
+           "roofline": roofline(r["alg_bytes_rank"], r["t_decode"], r["t_parse"], step_ms),
+           "with_gather": {"value": round(r["samples"] * steps / r["t_all"] / 1e6, 2), "unit": "MSamples/s",
+                           "ms_per_step": round(r["t_all"] / steps * 1e3, 4),
                            "note": "each step: decode, then shard.gather_bytes of every rank's PCM to rank 0"},
-           "with_gather_overlapped": {"value": round(r["samples"] * args.steps / r["t_ovl"] / 1e6, 2),
-                                      "unit": "MSamples/s", "ms_per_step": round(r["t_ovl"] / args.steps * 1e3, 4),
+           "with_gather_overlapped": {"value": round(r["samples"] * steps / r["t_ovl"] / 1e6, 2),
+                                      "unit": "MSamples/s", "ms_per_step": round(r["t_ovl"] / steps * 1e3, 4),
                                       "note": "step s's gather (shard.gather_post, RCCL send/recv) in flight while "
                                               "step s + 1 decodes into a second buffer; N = 1: no gather"}}
-    out["roofline"]["kernel"] = "k_parse + decode launch over the rank's files"
+    out["roofline"]["kernel"] = "decode launch over the rank's files (k_parse beside it: k_parse_avg_ms)"
+    out["roofline"]["parse_plus_decode_ms"] = round(r["t_launch"], 4)
     return out
 
 

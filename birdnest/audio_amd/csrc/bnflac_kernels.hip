@@ -2806,13 +2806,6 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  * mismatch, out-of-range samples, unsupported layouts) get BNF_FL_REDO and are decoded
  * again, exactly, by k_decode<8>, which runs after it on the same stream. */
 #define ST_CHK 16 /* samples per chunk (one 64-byte FLACDecoder run per frame) */
-/* CRC-16 from the rings while decoding (measured alternative, off: see below and DESIGN.md
- * section 9): 1 steps once per chunk, 2 inside the fused pairs.  0: the frame's bytes are
- * read again after the decode (st_crc16). */
-#ifndef BNF_ST_RING_CRC
-#define BNF_ST_RING_CRC 0
-#endif
-#define BNF_ST_CRC_PAIRS (BNF_ST_RING_CRC == 2)
 #ifndef BNF_ST_PAIR
 #define BNF_ST_PAIR 1 /* fused chunks decode Rice codewords two per window (st_fused_pair) */
 #endif
@@ -2827,7 +2820,6 @@ struct StCh {
     uint32_t esc, left, pidx, nparts, psamples, plen, pesc, porder, order;
     uint32_t wasted;
     int32_t lim, mx, mn; /* operand range of the path, sample range seen */
-    uint32_t crc, ca, ce; /* in-ring CRC-16: running value, next byte, end of the channel's range (absolute, mod 2^32) */
 };
 
 /* lo | hi << 16 from the low halves */
@@ -3176,58 +3168,6 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
     return crc;
 }
 
-/* ---- CRC-16 from the rings (read_frame_'s frame CRC, @0x10011a01).  The frame's bytes pass
- * through the two channel rings as they are decoded: channel 0's cursor walks [frame start,
- * X) and channel 1's [X, end) (X: the byte of subframe 1's first bit).  Each channel keeps a
- * running CRC over its range, advanced from the ring in 8-byte steps (slice-by-8 table, 4 KB
- * in LDS beside the rings) behind its decode cursor: a few steps per chunk, and before a
- * refill overwrites ring slots every byte in them is folded in.  Bytes the rings never hold
- * (the frame header, the words the cursor starts on) and the last few bytes go through
- * global memory; the two ranges are combined by a GF(2) shift (crc16_shift).  Round 2 read
- * the whole frame again after decoding it: ~11 GB of HBM reads per C2 step. */
-DEV uint32_t crc16_cont_global(uint32_t crc, const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1,
-                               const lds_u16 *T) {
-    uint64_t p = b0;
-    while (p < b1 && (p & 7u)) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xffu]) & 0xffffu; p++; }
-    while (p + 8u <= b1) {
-        const uint2 v = *(const uint2 *)(bytes + p);
-        crc = crc16_step8(crc, __builtin_bswap32(v.x), __builtin_bswap32(v.y), T);
-        p += 8u;
-    }
-    while (p < b1) { crc = ((crc << 8) ^ T[((crc >> 8) ^ bytes[p]) & 0xffu]) & 0xffffu; p++; }
-    return crc;
-}
-/* one 8-byte step of channel z's in-ring CRC (on: this lane steps) */
-DEV void st_crc_step(StCh &z, bool on, const lds_u16 *T) {
-    const uint32_t a = z.ca; /* absolute byte, 8-aligned */
-    const uint32_t off = ((a >> 4) & (ST_RD - 1u)) * (RING_LANE_DW * 4u) + (a & 8u);
-    const lds_u32 *q = z.b.lring + (off >> 2);
-    const uint32_t c = crc16_step8(z.crc, __builtin_bswap32(q[0]), __builtin_bswap32(q[1]), T);
-    z.crc = on ? c : z.crc;
-    z.ca += on ? 8u : 0u;
-}
-/* whether the ring still holds byte z.ca: a blocking refill (rare paths: landings, escapes)
- * may overwrite blocks before the CRC has passed them; those go through global memory */
-DEV bool st_crc_held(const StCh &z) { return (int32_t)(z.ca - ((z.b.iend - ST_RD) << 4)) >= 0; } /* mod 2^32 bytes */
-/* whether channel z's next CRC step is behind its decode cursor, inside its range and held */
-DEV bool st_crc_ready(const StCh &z) {
-    return (int32_t)((uint32_t)(br_pos(z.b) >> 3) - z.ca) >= 8 && (int32_t)(z.ce - z.ca) >= 8 && st_crc_held(z);
-}
-/* rare: a lane whose next CRC byte left the ring continues through global memory up to the
- * ring's oldest block (or the end of its range) */
-DEV void st_crc_lost(StCh &z, bool on, const uint8_t *bytes, uint64_t frame_off, uint32_t fo, const lds_u16 *T) {
-    if (on && (int32_t)(z.ce - z.ca) > 0 && !st_crc_held(z)) {
-        const uint32_t old = (z.b.iend - ST_RD) << 4;
-        const uint32_t to = (int32_t)(z.ce - old) < 0 ? z.ce : old;
-        z.crc = crc16_cont_global(z.crc, bytes, frame_off + (uint32_t)(z.ca - fo), frame_off + (uint32_t)(to - fo), T);
-        z.ca = to;
-    }
-}
-/* ... and whether it lies before byte b (mod 2^32) */
-DEV bool st_crc_before(const StCh &z, uint32_t b) {
-    return (int32_t)(b - z.ca) >= 8 && (int32_t)(z.ce - z.ca) >= 8 && st_crc_held(z);
-}
-
 /* Fused-path cursor (4-slot ring).  ra is the LDS byte offset of ring word wi inside the
  * channel's ring: bits 2-3 word in block, 4-9 lane, 10-11 slot.  Moving it one word on is
  * ((ra | 0x3F3) + c) & 0x1C0C | lane bits: the ones in bits 0-1 turn +c into +4, the ones in
@@ -3468,7 +3408,7 @@ template <int T, int FMT, int AS = -1>
 DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
                        uint32_t nq, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al,
                        uint32_t bs, bool store, u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1,
-                       uint32_t lane, bool anyw, const lds_u16 *CT) {
+                       uint32_t lane, bool anyw) {
     static_assert((T & 1) == 0, "pairs start on even samples");
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t spg = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u;
@@ -3492,11 +3432,6 @@ DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
     }
     st_lpc_out<T, FMT, AS>(z0, z1, u0a, u1a, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
     st_lpc_out<T + 1, FMT, AS>(z0, z1, u0b, u1b, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
-#if BNF_ST_CRC_PAIRS
-    /* one in-ring CRC step per pair, channels alternating: independent of the decode chain */
-    StCh &zc = ((T >> 1) & 1) ? z1 : z0;
-    st_crc_step(zc, st_crc_ready(zc), CT);
-#endif
 }
 
 /* One sample of both channels on the general path: warm-up, partition headers anywhere,
@@ -3542,10 +3477,6 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     /* 16 KB: both channels' bitstream rings; in the tail, the 20 KB CRC-16 field tables */
     __shared__ LDS_DMA_ALIGN uint32_t ring[(2 * ST_RD * RING_LANE_DW > CRC11_N / 2) ? 2 * ST_RD * RING_LANE_DW : CRC11_N / 2];
     static_assert((ST_RD * RING_LANE_DW * 4) % 1024 == 0, "channel 1's ring base must stay 1 KiB aligned (LDS-DMA)");
-#ifdef BNF_ST_PAD
-    __shared__ uint32_t occ_pad[BNF_ST_PAD]; /* experiment: LDS padding to cap waves per CU */
-    if (ablate == 0xDEADu) occ_pad[threadIdx.x] = 1u;
-#endif
     const uint32_t lane = threadIdx.x;
     const uint32_t slot = blockIdx.x * 64u + lane;
     const uint32_t f = (perm && slot < nframes) ? perm[slot] : slot; /* decode order (k_order) */
@@ -3571,11 +3502,6 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     uint8_t *dst = out + os * stride; /* the frame's first byte (planar: channel 0's) */
     const bool al = (((uintptr_t)dst) & 15u) == 0 && (FMT != BNF_OUT_PLANAR32 || (bs & 3u) == 0);
 
-    /* in-ring CRC: the slice-by-8 CRC-16 table behind the rings (16 KB + 4 KB) */
-    lds_u16 *CT = (lds_u16 *)((lds_u32 *)ring + 2 * ST_RD * RING_LANE_DW);
-    static_assert(2 * ST_RD * RING_LANE_DW + 8 * 256 / 2 <= (int)(sizeof(ring) / 4), "CRC table fits behind the rings");
-    if (BNF_ST_RING_CRC)
-        for (uint32_t i = lane; i < 8u * 256u / 2u; i += 64u) ((lds_u32 *)CT)[i] = ((const uint32_t *)&g_crc16_tab[0][0])[i];
     StCh z0, z1;
     lds_u32 *ring0 = (lds_u32 *)ring, *ring1 = (lds_u32 *)ring + ST_RD * RING_LANE_DW;
     br_init(z0.b, words, nbytes, ring0, lane, ST_RD);
@@ -3610,28 +3536,6 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     const uint32_t nchunks = (mybs + ST_CHK - 1) / ST_CHK;
     uint32_t trunc = 0;
     wait_vm(); /* setup loads done: the store count starts from zero */
-    if (BNF_ST_RING_CRC) lds_sync(); /* the CRC table is in LDS */
-    /* in-ring CRC setup: each channel's range up to the oldest ring byte (8-aligned) through
-     * global memory, the rest from the ring */
-    const uint64_t fbit = fi.frame_off * 8u;
-    const uint32_t fo = (uint32_t)fi.frame_off;
-    const bool crc_ring = BNF_ST_RING_CRC && ok && !(ablate & (1u | BNF_MODE_DEFER_CRC));
-    const uint64_t xabs = ok ? (fbit + fi.sub_start[1]) >> 3 : 0ull;
-    z0.crc = z1.crc = 0u;
-    z0.ca = z1.ca = z0.ce = z1.ce = 0u; /* ce == ca: no steps */
-    if (BNF_ST_RING_CRC && crc_ring) {
-        const uint8_t *bytes = (const uint8_t *)words;
-        const uint64_t o0 = max((uint64_t)(z0.b.iend - ST_RD) * 16u, (fi.frame_off + 7u) & ~(uint64_t)7u);
-        const uint64_t s0 = min(o0, xabs);
-        z0.crc = crc16_cont_global(0u, bytes, fi.frame_off, s0, CT);
-        z0.ca = (uint32_t)s0;
-        z0.ce = (uint32_t)xabs;
-        const uint64_t s1 = max((uint64_t)(z1.b.iend - ST_RD) * 16u, (xabs + 7u) & ~(uint64_t)7u);
-        z1.crc = crc16_cont_global(0u, bytes, xabs, s1, CT);
-        z1.ca = (uint32_t)s1;
-        z1.ce = z1.ca + 0x40000000u;
-        wait_vm();
-    }
     uint32_t nst = 0; /* vector-memory ops (PCM stores) issued by this wave since the last refill's DMAs */
     const uint64_t t_loop = tnow(tmon);
     for (uint32_t kc = 0; kc < nchunks; kc++) {
@@ -3664,7 +3568,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                         const uint32_t nb = n0 + g * 8u;
                         const bool sto = !(ablate & 2u);
 #if BNF_ST_PAIR
-#define FPAIR(T) st_fused_pair<T, FMT, AS>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw, CT)
+#define FPAIR(T) st_fused_pair<T, FMT, AS>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
                         FPAIR(0); FPAIR(2); FPAIR(4); FPAIR(6);
 #undef FPAIR
 #else
@@ -3711,30 +3615,6 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
          * stays in flight), then issue the next blocks; the flush's stores are younger */
         {
             const bool want = valid && n0 + ST_CHK < bs;
-            if (BNF_ST_RING_CRC && any_lane(crc_ring)) { /* in-ring CRC: the fused pairs step it; here bytes a blocking refill took, the
-                                       * rest of a general chunk, then the slots this refill overwrites */
-                if (__builtin_expect(any_lane(crc_ring && !(st_crc_held(z0) && st_crc_held(z1))), 0)) {
-                    st_crc_lost(z0, crc_ring, (const uint8_t *)words, fi.frame_off, fo, CT);
-                    st_crc_lost(z1, crc_ring, (const uint8_t *)words, fi.frame_off, fo, CT);
-                }
-#pragma unroll
-                for (int t = 0; t < 3; t++) {
-                    const bool c0 = st_crc_ready(z0), c1 = st_crc_ready(z1);
-                    if (!any_lane(c0 || c1)) break;
-                    st_crc_step(z0, c0, CT);
-                    st_crc_step(z1, c1, CT);
-                }
-                const uint32_t g0 = ((z0.b.wi >> 2) & ~3u) + 4u, g1 = ((z1.b.wi >> 2) & ~3u) + 4u;
-                /* a refilling lane's old group [iend - 8, iend - 4) blocks must be folded in first */
-                const uint32_t b0 = (z0.b.iend - 4u) << 4, b1 = (z1.b.iend - 4u) << 4;
-                const bool r0 = want && z0.b.iend == g0, r1 = want && z1.b.iend == g1;
-                for (;;) {
-                    const bool c0 = r0 && st_crc_before(z0, b0), c1 = r1 && st_crc_before(z1, b1);
-                    if (!any_lane(c0 || c1)) break;
-                    st_crc_step(z0, c0, CT);
-                    st_crc_step(z1, c1, CT);
-                }
-            }
             wait_vm_n(nst);
             z0.b.vendw = z0.b.iend * 4u;
             z1.b.vendw = z1.b.iend * 4u;
@@ -3785,14 +3665,6 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
      * of a batch, a gap before the next offset, a mismatch) the frame is re-read here. */
     uint32_t crc = crc_read;
     const bool defer = (ablate & BNF_MODE_DEFER_CRC) != 0; /* k_crc_join checks it */
-#if BNF_ST_RING_CRC
-    if (ok && crc_ring) { /* the in-ring CRC's last bytes (the lag behind each cursor) through global memory */
-        const uint8_t *bytes = (const uint8_t *)words;
-        const uint32_t c0 = crc16_cont_global(z0.crc, bytes, fi.frame_off + (uint32_t)(z0.ca - fo), xabs, CT);
-        const uint32_t c1 = crc16_cont_global(z1.crc, bytes, fi.frame_off + (uint32_t)(z1.ca - fo), end_byte, CT);
-        crc = crc16_shift(c0, end_byte - xabs) ^ c1;
-    }
-#else
     bool need = false;
     if (ok && !defer) {
         const uint32_t cn = info[f].crc_next;
@@ -3806,7 +3678,6 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         __syncthreads();
         if (need) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
     }
-#endif
     if (ok && crc != crc_read) ok = false;
     if (ok) {
         info[f].resume_bit = resume;
@@ -5104,8 +4975,15 @@ static bool use_decode_wave(uint32_t nframes, uint32_t cmax, uint32_t bsmax) {
     return DW_AUTO && nframes <= 2u * cus * wpc;
 }
 
-/* k_decode_sys (systolic restore, every frame class) or the lane kernels by class.
+/* k_decode_sys (systolic restore, every frame class) or the lane kernels by class.  The lane
+ * kernels run one subframe per lane (k_decode_st: one stereo frame), so a launch of few frames is
+ * a few waves, each as long as one lane's serial chain; k_decode_sys spreads each subframe over a
+ * producer lane and a restore quad.  Auto: k_decode_sys while the lane kernels would have fewer
+ * than SYS_AUTO_WAVES subframe waves (BNFLAC_SYS_WAVES overrides).
  * BNFLAC_DECODE_SYS=0 never, 1 always; bnf_set_decode_sys overrides. */
+#ifndef SYS_AUTO_WAVES
+#define SYS_AUTO_WAVES 1024u
+#endif
 static std::atomic<int> g_decode_sys{-1};
 static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32_t chn_lanes) {
     int m = g_decode_sys.load(std::memory_order_relaxed);
@@ -5114,10 +4992,15 @@ static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32
         m = e ? (atoi(e) ? 1 : 0) : 2;
         g_decode_sys.store(m, std::memory_order_relaxed);
     }
-    (void)nframes;
     (void)sp;
-    if (chn_lanes > 8u) return false;
-    return m == 1;
+    if (chn_lanes > 8u || m == 0) return false;
+    if (m == 1) return true;
+    if (g_decode_wave.load(std::memory_order_relaxed) == 1) return false; /* k_decode_wave forced */
+    static const uint32_t lim = [] {
+        const char *e = getenv("BNFLAC_SYS_WAVES");
+        return e ? (uint32_t)strtoul(e, nullptr, 0) : SYS_AUTO_WAVES;
+    }();
+    return (uint64_t)nframes * chn_lanes < (uint64_t)lim * 64u;
 }
 
 extern "C" {

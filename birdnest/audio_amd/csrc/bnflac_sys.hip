@@ -94,18 +94,16 @@ DEV uint64_t sys_now(bool on) {
 struct SysQ {
     uint32_t d0, d1, d2;
     uint32_t e0, e1, e2;
+    uint64_t tw, dw; /* stats mode: wait cycles, DMA instructions waited past (flushed once per wave) */
 };
 __device__ unsigned long long g_sys_dbg[4]; /* debug: refill wait cycles, DMA instructions (stats mode) */
 DEV void sys_refill(BR &b, bool want, SysQ &q, bool tm = false) {
     const uint64_t tw = tm ? __builtin_amdgcn_s_memtime() : 0ull;
     wait_vm_n(q.d0 + q.d1 + q.d2);
-    if (tm) {
+    if (tm) { /* no global atomics here: their vmcnt wait would drain the DMAs in flight */
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint64_t dt = __builtin_amdgcn_s_memtime() - tw;
-        if ((threadIdx.x & 63u) == 0u) {
-            atomicAdd(&g_sys_dbg[0], dt);
-            atomicAdd(&g_sys_dbg[1], (unsigned long long)(q.d0 + q.d1 + q.d2));
-        }
+        q.tw += __builtin_amdgcn_s_memtime() - tw;
+        q.dw += q.d0 + q.d1 + q.d2;
     }
     b.vendw = max(b.vendw, q.e2 * 4u); /* issued before the refill three back: landed */
     q.e2 = q.e1;
@@ -177,44 +175,163 @@ DEV void sys_rare(BR &b, bool sl, bool ld, uint32_t k, uint32_t (&u)[NW], uint64
     }
 }
 /* SYS_HALF Rice codewords of one partition (parameter k; km = 31 - k, k1 = k + 1, k32 = 32 - k),
- * unchecked except for a landing test every other step, into registers.  PAIR: two codewords per
- * 32-bit window (small k: C2's ~10-bit codewords) with one advance and one ring read. */
+ * unchecked except for a landing test per step, into registers.  PAIR: two codewords per 32-bit
+ * window (small k: C2's ~10-bit codewords) with one advance.  A step moves the window by at most
+ * one word, so the word entering it at step T + 2 is the one after the window's at step T + 1 or
+ * the one after that: the ring read of the latter is issued at the end of step T and selected at
+ * step T + 2 (nw = c ? z : nw), a step and a half after its issue -- the LDS latency is off the
+ * cursor chain, which the single-read-per-advance form (br_adv) waits for every step. */
 template <bool PAIR>
 DEV void sys_rice_run(BR &b, bool on, uint32_t k, uint32_t km, uint32_t k1, uint32_t k32, int32_t (&r)[SYS_HALF],
                       uint64_t limit, uint32_t &trunc, uint32_t lane) { /* on: this lane decodes (others stand still) */
     const uint32_t laneb = lane << 4;
     sys_resync(b, lane);
+    /* nw: ring[wi] at this step (the word entering at a crossing); z1 / z2: ring[wi + 1] as issued
+     * at the end of the last step / the one before; cprev: the last step crossed.  Then
+     * nw(T) = c(T-1) ? z(T-2) : nw(T-1) -- z(T-2) was issued a step and a half earlier. */
+    if (__builtin_expect(any_lane(on && b.wi + 1u >= b.vendw), 0)) {
+        wait_vm();
+        b.vendw = b.iend * 4u;
+        if (b.wi + 1u >= b.vendw) {
+            br_refill(b);
+            wait_vm();
+            br_drained(b);
+        }
+        sys_resync(b, lane);
+        sys_next_word(b);
+    }
+    uint32_t nw = b.nx, cprev = 0, z2 = 0, z1;
+    {
+        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & 0x3C0Cu) | laneb;
+        z1 = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + ra1);
+    }
 #pragma unroll
     for (int T = 0; T < SYS_HALF; T += PAIR ? 2 : 1) {
+        nw = cprev ? z2 : nw;
         const uint32_t w = br_peek(b);
+        uint32_t u[2], n;
+        bool sl;
         if (PAIR) {
-            uint32_t u[2];
             const uint32_t qa = min(ffbh(w), 32u);
             const uint32_t la = qa + k1;
             const uint32_t w2 = w << (la & 31u);
             const uint32_t qb = min(ffbh(w2), 32u);
             u[0] = (qa << k) | __builtin_amdgcn_ubfe(w, km - qa, k);
             u[1] = (qb << k) | __builtin_amdgcn_ubfe(w2, km - qb, k);
-            const uint32_t n = la + qb + k1;
-            const bool sl = on && n > 32u;
-            sys_adv(b, (sl || !on) ? 0u : n, laneb);
-            const bool ld = on && (T & 2) == 0 && b.wi >= b.vlim;
-            sys_next_word(b);
-            if (__builtin_expect(any_lane(sl || ld), 0)) sys_rare<2>(b, sl, ld, k, u, limit, trunc, lane);
-            r[T] = sys_zz(u[0]);
-            r[T + 1] = sys_zz(u[1]);
+            n = la + qb + k1;
+            sl = on && n > 32u;
         } else {
-            uint32_t u[1];
             const uint32_t q = ffbh(w); /* ~0u for an empty window: slow */
-            const bool sl = on && q >= k32;
             u[0] = (q << k) | __builtin_amdgcn_ubfe(w, km - q, k);
-            sys_adv(b, (sl || !on) ? 0u : q + k1, laneb);
-            const bool ld = on && (T & 1) == 0 && b.wi >= b.vlim;
-            sys_next_word(b);
-            if (__builtin_expect(any_lane(sl || ld), 0)) sys_rare<1>(b, sl, ld, k, u, limit, trunc, lane);
-            r[T] = sys_zz(u[0]);
+            n = q + k1;
+            sl = on && q >= k32;
         }
+        /* advance (the window crosses at most one word) */
+        uint32_t t;
+        bool c = __builtin_usub_overflow(b.s, (sl || !on) ? 0u : n, &t);
+        b.s = t & 31u;
+        b.hi = c ? b.lo : b.hi;
+        b.lo = c ? __builtin_bswap32(nw) : b.lo;
+        b.wi += (uint32_t)c;
+        b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x3C0Cu) | laneb;
+        const bool ld = on && b.wi + 1u >= b.vendw; /* the read below must hit landed words */
+        if (__builtin_expect(any_lane(sl || ld), 0)) {
+            b.nx = c ? z1 : nw; /* the generic reader's ring[wi] */
+            if (any_lane(ld)) {
+                STAT(b.stats, 2);
+                wait_vm();
+                b.vendw = b.iend * 4u;
+                if (b.wi + 1u >= b.vendw) {
+                    br_refill(b);
+                    wait_vm();
+                    br_drained(b);
+                }
+                sys_resync(b, lane);
+                sys_next_word(b);
+            }
+            if (any_lane(sl)) {
+                STAT(b.stats, 3);
+                if (sl) {
+#pragma unroll
+                    for (int i = 0; i < (PAIR ? 2 : 1); i++) {
+                        uint32_t qq;
+                        if (!br_unary(b, qq, limit)) trunc = 1;
+                        u[i] = (qq << k) | br_read(b, k);
+                    }
+                }
+                sys_resync(b, lane);
+            }
+            nw = b.nx; /* ring[wi]: the next step reads it as nw(T + 1) */
+            c = false;
+        }
+        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & 0x3C0Cu) | laneb;
+        const uint32_t zn = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + ra1);
+        z2 = z1;
+        z1 = zn;
+        cprev = c;
+        r[T] = sys_zz(u[0]);
+        if (PAIR) r[T + 1] = sys_zz(u[1]);
     }
+    b.nx = cprev ? z2 : nw; /* the generic reader's ring[wi] */
+}
+
+/* The same run as one straight line (no branch inside, so the compiler can count the LDS reads in
+ * flight instead of draining them at every merge): the caller has made sure every word the run
+ * can reach has landed (wi + 2 + SYS_HALF words), each residual is written to the lane's row as
+ * it is decoded, and a lane whose codeword (pair) does not fit the 32-bit window freezes its
+ * cursor there.  Returns the codewords decoded (SYS_HALF unless frozen); the caller finishes a
+ * frozen lane's run with the generic reader. */
+template <bool PAIR>
+DEV uint32_t sys_rice_line(BR &b, bool on, uint32_t k, uint32_t km, uint32_t k1, uint32_t k32, int32_t *row,
+                           uint32_t lane) {
+    const uint32_t laneb = lane << 4;
+    sys_resync(b, lane);
+    uint32_t nw = b.nx, cprev = 0, z2 = 0, z1, cnt = 0;
+    bool frozen = !on;
+    {
+        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & 0x3C0Cu) | laneb;
+        z1 = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + ra1);
+    }
+#pragma unroll
+    for (int T = 0; T < SYS_HALF; T += PAIR ? 2 : 1) {
+        nw = cprev ? z2 : nw;
+        const uint32_t w = br_peek(b);
+        uint32_t u0, u1 = 0, n;
+        bool sl;
+        if (PAIR) {
+            const uint32_t qa = min(ffbh(w), 32u);
+            const uint32_t la = qa + k1;
+            const uint32_t w2 = w << (la & 31u);
+            const uint32_t qb = min(ffbh(w2), 32u);
+            u0 = (qa << k) | __builtin_amdgcn_ubfe(w, km - qa, k);
+            u1 = (qb << k) | __builtin_amdgcn_ubfe(w2, km - qb, k);
+            n = la + qb + k1;
+            sl = n > 32u;
+        } else {
+            const uint32_t q = ffbh(w); /* ~0u for an empty window: slow */
+            u0 = (q << k) | __builtin_amdgcn_ubfe(w, km - q, k);
+            n = q + k1;
+            sl = q >= k32;
+        }
+        frozen = frozen || sl;
+        uint32_t t;
+        const bool c = __builtin_usub_overflow(b.s, frozen ? 0u : n, &t);
+        b.s = t & 31u;
+        b.hi = c ? b.lo : b.hi;
+        b.lo = c ? __builtin_bswap32(nw) : b.lo;
+        b.wi += (uint32_t)c;
+        b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x3C0Cu) | laneb;
+        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & 0x3C0Cu) | laneb;
+        const uint32_t zn = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + ra1);
+        z2 = z1;
+        z1 = zn;
+        cprev = c;
+        row[T * SYS_RP] = sys_zz(u0); /* a frozen lane's are rewritten by the caller */
+        if (PAIR) row[(T + 1) * SYS_RP] = sys_zz(u1);
+        cnt += frozen ? 0u : (PAIR ? 2u : 1u);
+    }
+    b.nx = cprev ? z2 : nw; /* the generic reader's ring[wi] */
+    return cnt;
 }
 
 /* ------------------------------------------------------------------ the restore quad */
@@ -459,7 +576,7 @@ DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt,
     const uint64_t cofs = (uint64_t)(n0 / SYS_CHK) * k.cbytes;
 #pragma unroll
     for (int r = 0; r < 2; r++) {
-        if (!any_lane(k.pv[r])) break;
+        if (!any_lane(k.pv[r] && n0 < k.bs[r])) continue; /* piece 0's frame may be out while piece 1's decodes */
         if (!k.pv[r] || n0 >= k.bs[r]) continue;
         uint32_t s0 = k.s0[r], p = k.p[r];
         const uint32_t as = k.as[r];
@@ -761,10 +878,15 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         SysQ q;
         q.d0 = q.d1 = q.d2 = 0;
         q.e0 = q.e1 = q.e2 = b.iend;
+        q.tw = q.dw = 0;
         sys_bar(); /* B0: tables ready */
         /* ================================================= producer: chunks */
         const bool tm = b.stats;
         uint64_t t_ref = 0, t_dec = 0, t_bar = 0;
+        /* the wave's largest Rice parameter (selects the PAIR run), reduced again only after a
+         * partition header: an upper bound for the lanes of a run, which only costs the pairing */
+        uint32_t kmax = 0;
+        bool kdirty = true;
         for (uint32_t k = 0; k <= nchunks; k++) {
             if (k < nchunks) {
                 const uint32_t n0 = k * SYS_CHK;
@@ -782,13 +904,40 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                     const bool run = active && h0 + SYS_HALF <= bs && h0 >= order;
                     if (any_lane(run && rs.left == 0u && rs.pidx < rs.nparts)) {
                         if (run && rs.left == 0u && rs.pidx < rs.nparts) read_partition(b, rs);
+                        kdirty = true;
                     }
                     const bool fast = !(ablate & 0x200000u) && !any_lane(active && h0 < bs && !(run && !rs.esc && rs.left >= SYS_HALF));
-                    if (fast && any_lane(run)) {
+                    if (fast && any_lane(run) && kdirty) {
+                        kmax = active ? rs.k : 0u;
+                        for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor(kmax, o));
+                        kdirty = false;
+                    }
+                    if (fast && any_lane(run) && !(ablate & 0x800000u)) {
+                        const uint32_t kk = run ? rs.k : 0u;
+                        /* every word the run can reach has landed */
+                        if (__builtin_expect(any_lane(run && b.wi + 2u + SYS_HALF >= b.vendw), 0)) {
+                            STAT(b.stats, 2);
+                            wait_vm();
+                            b.vendw = b.iend * 4u;
+                            if (b.wi + 2u + SYS_HALF >= b.vendw) {
+                                br_refill(b);
+                                wait_vm();
+                                br_drained(b);
+                            }
+                            b.nx = ring_word(b, b.wi);
+                        }
+                        int32_t *rrow = row + (h0 - n0) * SYS_RP;
+                        const uint32_t got = kmax <= 9u ? sys_rice_line<true>(b, run, kk, 31u - kk, kk + 1u, 32u - kk, rrow, lane)
+                                                        : sys_rice_line<false>(b, run, kk, 31u - kk, kk + 1u, 32u - kk, rrow, lane);
+                        if (__builtin_expect(any_lane(run && got < SYS_HALF), 0)) { /* frozen lanes: the generic reader */
+                            STAT(b.stats, 3);
+                            if (run)
+                                for (uint32_t i = got; i < SYS_HALF; i++) rrow[i * SYS_RP] = rice_one<true>(b, kk, limit, trunc);
+                        }
+                        if (run) rs.left -= SYS_HALF;
+                    } else if (fast && any_lane(run)) {
                         int32_t r[SYS_HALF];
                         const uint32_t kk = run ? rs.k : 0u;
-                        uint32_t kmax = kk;
-                        for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor(kmax, o));
                         if (kmax <= 9u) sys_rice_run<true>(b, run, kk, 31u - kk, kk + 1u, 32u - kk, r, limit, trunc, lane);
                         else sys_rice_run<false>(b, run, kk, 31u - kk, kk + 1u, 32u - kk, r, limit, trunc, lane);
                         if (run) {
@@ -797,6 +946,7 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                             for (int i = 0; i < SYS_HALF; i++) row[(h0 - n0 + (uint32_t)i) * SYS_RP] = r[i];
                         }
                     } else {
+                        kdirty = true; /* rice_fused may read partition headers */
                         const uint32_t lo = max(h0, order), hi = active ? min(h0 + SYS_HALF, bs) : 0u;
                         if (ablate & 8u) {
                             for (uint32_t n = lo; n < hi; n++) row[(n - n0) * SYS_RP] = 0;
@@ -817,6 +967,8 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             atomicAdd(&g_stats[8], (unsigned long long)t_ref);
             atomicAdd(&g_stats[9], (unsigned long long)t_dec);
             atomicAdd(&g_stats[10], (unsigned long long)t_bar);
+            atomicAdd(&g_sys_dbg[0], (unsigned long long)q.tw);
+            atomicAdd(&g_sys_dbg[1], (unsigned long long)q.dw);
         }
         /* ================================================= producer: tail (read_frame_ @0x100118c0) */
         const bool last = active && ch + 1u == fi.channels;

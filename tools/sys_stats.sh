@@ -1,6 +1,6 @@
 set -u
 for cfg in "C5 --c5-batch" "C2 --batches 64"; do
-  for ab in 0x100 0x80100; do
+  for ab in 0x100 0x800100; do
     BNFLAC_DECODE_SYS=1 BNFLAC_ABLATE=$ab timeout -k 10 200 python3 bench.py --config $cfg --steps 3 --warmup 1 --legs= --no-cpu-baseline --no-pcie --no-index --no-reader --stats > gpurun_out/stx.json 2>&1 || { tail -5 gpurun_out/stx.json; exit 1; }
     python3 -c "
 import json
