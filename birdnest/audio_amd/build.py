@@ -40,7 +40,7 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-KERNEL_TUS = (0, 1, 2, 3, 4, 5, 6, 7)  # one build of bnflac_kernels.hip per BNF_TU: scan+parse, k_decode<8>, k_decode<32>, k_decode_st<FLACDECODER>, k_decode_st<others>, k_decode<16>, k_decode_wave, k_decode_sw
+KERNEL_TUS = (0, 1, 2, 3, 4, 5, 7)  # one build of bnflac_kernels.hip per BNF_TU: scan+parse, k_decode<8>, k_decode<32> + k_decode_list, k_decode_st<FLACDECODER>, k_decode_st<others>, k_decode<16>, k_decode_sw (TU 8: bnflac_sys.hip)
 
 
 def build_hip(force=False, verbose=False):

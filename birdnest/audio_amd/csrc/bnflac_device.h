@@ -56,7 +56,7 @@ enum {
     BNF_FL_REDO = 64u,         /* set by k_decode_st: declined (rare case), decoded again by k_decode<8> */
     BNF_FL_W16 = 128u,         /* set by k_parse: LPC orders 9..16, or LPC above 16 bits (k_decode<16>) */
     BNF_FL_CRC_DEFER = 256u,   /* decoded with the CRC-16 check left to k_crc_join (concurrent CRC pass) */
-    BNF_FL_WAVE_REDO = 512u,   /* set by k_decode_wave: wider than its rows, decoded by the lane kernels */
+    BNF_FL_WAVE_REDO = 512u,   /* set by k_decode_sys: handed back, decoded again by k_decode_list */
     BNF_FL_SW = 1024u          /* set by k_parse: 2-channel W16 frame of 17..24 bits, LPC orders <= 12 (k_decode_sw's candidates) */
 };
 

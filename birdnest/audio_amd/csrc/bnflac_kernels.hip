@@ -105,7 +105,7 @@ DEV void gst128(uint64_t addr, u32x4 v) { *(__attribute__((address_space(1))) u3
  * ablation): the decode kernels leave the CRC-16 check to k_crc_join, because the
  * concurrent CRC pass (k_crc, on a second stream) is still running. */
 #define BNF_MODE_DEFER_CRC 0x1000u
-/* Mode bit: the lane kernels decode only the frames k_decode_wave handed back (BNF_FL_WAVE_REDO). */
+/* Mode bit: the lane kernel decodes only the frames k_decode_sys handed back (BNF_FL_WAVE_REDO). */
 #define BNF_MODE_WREDO 0x4000u
 /* Mode bit: k_decode_sw ran before the other lane kernels (they take its SW frames only when
  * it handed them back).  Host ablation bit BNF_ABLATE_NO_SW: do not launch it. */
@@ -931,7 +931,8 @@ DEV uint32_t seg_walk(const uint32_t (&w)[SW + 1], uint32_t pos, uint32_t k1, ui
     }
     return pos;
 }
-/* DEC: also decode the codewords (k_decode_wave): the values of the partition's codewords go
+/* DEC: also decode the codewords (a wave-cooperative residual decode; round 3's k_decode_wave
+ * used it, nothing does now): the values of the partition's codewords go
  * to dst[0 .. cnt) (zig-zag decoded, libFLAC's 32-bit unsigned (q << k) | lsb) -- each lane
  * decodes the codewords whose starts its walk recorded, their lengths known from the next
  * start, the k low bits read from the ring. */
@@ -1094,7 +1095,7 @@ DEV bool wave_rice_skip_any(WR &r, uint32_t cnt, uint32_t k, uint64_t limit, boo
     default: return wave_rice_skip<16>(r, cnt, k, limit, stats);
     }
 }
-/* k_decode_wave's partition decode: the pass width as wave_rice_skip_any */
+/* a partition decode (DEC) at the pass width wave_rice_skip_any picks */
 DEV bool wave_rice_dec_any(WR &r, uint32_t cnt, uint32_t k, uint64_t limit, int32_t *dst) {
     const uint32_t est = cnt * (k + 2u);
     const int sw = est > 6u * 2048u ? 16 : est > 3u * 2048u ? 8 : est > 3u * 1024u ? 4 : est > 1536u ? 2 : 1;
@@ -2145,7 +2146,7 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
 
     bnf_frame_info fi;
     bool have = (fl < fpb) && (slot < nframes);
-    if (ablate & BNF_MODE_WREDO) have = have && (info[f].flags & BNF_FL_WAVE_REDO); /* after k_decode_wave: its hand-backs */
+    if (ablate & BNF_MODE_WREDO) have = have && (info[f].flags & BNF_FL_WAVE_REDO); /* after k_decode_sys: its hand-backs */
     /* k_decode_sw's frames (BNF_MODE_SW: it ran first) are this kernel's only once handed back */
     const bool sw_on = (ablate & BNF_MODE_SW) != 0;
     const bool lst = (ablate & BNF_MODE_LIST) != 0; /* k_decode_list: every frame of the list is this instance's */
@@ -4300,396 +4301,6 @@ hipError_t bnf_launch_decode_sw_tu7(const uint32_t *words, uint64_t nbytes, uint
 } /* extern "C" */
 #endif
 
-#if BNF_TU == 6
-/* ============================================================ k_decode_wave
- * One wave per frame for launches too small to fill the chip with lane-per-frame waves (a
- * stream's reader window, one 10 s C5 file): the frame's latency is then the whole launch's,
- * and a lane walking 4,096 codewords and MACs alone is ~1 ms.  Per channel the wave reads the
- * subframe header at the uniform cursor and decodes the residual with the wave-cooperative
- * Rice scan (wave_rice_skip<SW, true>: every lane decodes the codewords of its own stream
- * segment) into the frame's sample rows in LDS; the restore runs one lane per channel (C
- * lanes side by side, the k_decode predictor: MMX16 / ia32 / wide exactly); the CRC-16 is
- * split over the 64 lanes; decorrelation and the output layout are written by all lanes,
- * coalesced.  Same records and output bytes as the lane kernels for every frame whose status
- * is OK (a frame that turns out TRUNC / ERROR in its last subframe gets its record; its PCM
- * is not written).  A frame wider than the launch's rows (channels, blocksize above
- * STREAMINFO's) is flagged BNF_FL_WAVE_REDO and left to the lane kernels. */
-#define DW_TAB 16 /* header words per channel */
-struct DwHdr { /* a channel's restore parameters (LDS table) */
-    uint32_t type, order, wasted, path;
-    int32_t shift, cval;
-};
-/* The restore of one channel on one lane (k_decode's exact predictor, pred_at).  The taps
- * oldest first in four MAC chains and the newest tap last (the older taps' MACs issue while the
- * previous sample is still being computed), the chains kept apart by an opaque non-volatile
- * asm (the compiler would re-associate them into one chain; a volatile one also pinned the LDS
- * loads behind it).  N24: libFLAC's 32-bit paths (ia32, MMX16, FIXED, CONSTANT) want the low 32
- * bits of the sum, which v_mad_i32_i24 gives exactly while every history value fits 24 bits
- * (coefficients always do: qlp precision <= 15); a group of W samples that leaves that range
- * is restored again with the 64-bit MACs, which the channel keeps from then on. */
-template <int T, int W, bool N24>
-DEV int32_t dw_pred(const int32_t (&c)[W], const int32_t (&x)[W], const int32_t (&xt)[4], const Pred &p) {
-    if constexpr (N24) {
-        int32_t a[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int u = 0; u < W - 1; u++) {
-            const int t = W - 1 - u;
-            const int32_t hv = (t < 4) ? xt[(T - 1 - t) & 3] : x[((T - 1 - t) % W + W) % W];
-            a[t & 3] = (int32_t)((uint32_t)a[t & 3] + (uint32_t)__mul24(c[t], hv));
-        }
-        asm("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
-        const uint32_t S = ((uint32_t)a[0] + (uint32_t)a[1]) + ((uint32_t)a[2] + (uint32_t)a[3]) +
-                           (uint32_t)__mul24(c[0], xt[(T - 1) & 3]);
-        return (int32_t)S >> p.sh;
-    } else {
-        int64_t a[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int u = 0; u < W - 1; u++) { /* taps W-1 .. 1: samples older than the newest */
-            const int t = W - 1 - u;
-            const int32_t hv = (t < 4) ? xt[(T - 1 - t) & 3] : x[((T - 1 - t) % W + W) % W];
-            a[t & 3] += (int64_t)c[t] * (int64_t)hv;
-        }
-        asm("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
-        const int64_t S = ((a[0] + a[1]) + (a[2] + a[3])) + (int64_t)c[0] * (int64_t)xt[(T - 1) & 3]; /* newest last */
-        return p.wide ? (int32_t)(S >> p.sh) : ((int32_t)S >> p.sh);
-    }
-}
-template <int T, int W, bool N24>
-DEV void dw_restore_steps(int32_t *buf, const int32_t (&v)[W], const int32_t (&c)[W], int32_t (&x)[W], int32_t (&xt)[4],
-                          const Pred &p, uint32_t j, uint32_t &oor) {
-    if constexpr (T < W) {
-        const int32_t pr = dw_pred<T, W, N24>(c, x, xt, p);
-        const int32_t s = (j + (uint32_t)T < p.order) ? v[T] : (int32_t)((uint32_t)v[T] + (uint32_t)pr);
-        if (N24) oor |= ((uint32_t)s + 0x800000u) >> 24; /* s outside [-2^23, 2^23) */
-        push_at<T, W>(x, xt, p, s);
-        buf[j + T] = (int32_t)((uint32_t)s << p.wasted); /* rows past bs are padding: no branch between samples */
-        dw_restore_steps<T + 1, W, N24>(buf, v, c, x, xt, p, j, oor);
-    }
-}
-/* lane ch < C restores its channel's rows in place (residuals / warm-ups in, samples out);
- * called by those lanes only (the range test is a ballot over them) */
-template <int W>
-DEV void dw_restore(int32_t *buf, uint32_t bs, const int32_t *ctab, const DwHdr &h) {
-    int32_t c[W], x[W], xt[4];
-#pragma unroll
-    for (int t = 0; t < W; t++) { c[t] = 0; x[t] = 0; }
-#pragma unroll
-    for (int t = 0; t < 4; t++) xt[t] = 0;
-    Pred pd;
-    pd.order = h.order;
-    pd.wasted = h.wasted;
-    pd.sh = 0;
-    pd.mmx = false;
-    pd.wide = false;
-    if (h.type == T_LPC) {
-#pragma unroll
-        for (int t = 0; t < W; t++) c[t] = ((uint32_t)t < h.order) ? ctab[t] : 0;
-        pd.mmx = h.path == P_MMX16;
-        pd.wide = h.path == P_WIDE;
-        if (h.path == P_MMX16) pd.sh = ((uint32_t)h.shift >= 32u) ? 31 : h.shift;
-        else if (h.path == P_IA32) pd.sh = h.shift & 31;
-        else pd.sh = min((uint32_t)h.shift & 0xFFu, 63u);
-    } else if (h.type == T_FIXED) {
-        const uint32_t o = h.order;
-        c[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
-        c[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
-        c[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
-        c[3] = o == 4 ? -1 : 0;
-    } else if (h.type == T_CONST) {
-        c[0] = 1;
-        pd.order = 1;
-    }
-    bool n24 = !any_lane(pd.wide); /* the 64-bit path needs the exact sum */
-#pragma unroll 1
-    for (uint32_t j = 0; j < bs; j += W) {
-        int32_t v[W];
-#pragma unroll
-        for (int t = 0; t < W; t++) v[t] = buf[j + t];
-        uint32_t oor = 0;
-        if (n24) {
-            int32_t x0[W], xt0[4];
-#pragma unroll
-            for (int t = 0; t < W; t++) x0[t] = x[t];
-#pragma unroll
-            for (int t = 0; t < 4; t++) xt0[t] = xt[t];
-            dw_restore_steps<0, W, true>(buf, v, c, x, xt, pd, j, oor);
-            if (!any_lane(oor != 0u)) continue;
-            n24 = false; /* a value left 24 bits: this group again, exactly, and the rest too */
-#pragma unroll
-            for (int t = 0; t < W; t++) x[t] = x0[t];
-#pragma unroll
-            for (int t = 0; t < 4; t++) xt[t] = xt0[t];
-        }
-        dw_restore_steps<0, W, false>(buf, v, c, x, xt, pd, j, oor);
-    }
-}
-
-__global__ void __launch_bounds__(64) k_decode_wave(const uint32_t *__restrict__ words, uint64_t nbytes, uint32_t nframes,
-                                                    bnf_stream_params sp, int fmt, uint8_t *__restrict__ out,
-                                                    uint64_t out_bytes, bnf_frame_info *__restrict__ info, uint32_t cmax,
-                                                    uint32_t bsmax, uint32_t ablate) {
-    __shared__ LDS_DMA_ALIGN uint32_t ring[WR_SLOTS * WR_WIN];
-    __shared__ uint16_t tabs[8 * 256];         /* CRC-16 slice-by-8 */
-    __shared__ int32_t ctab[8 * 32];           /* LPC coefficients per channel */
-    __shared__ uint32_t htab[8 * DW_TAB];      /* DwHdr per channel */
-    extern __shared__ int32_t rows[];          /* channel c's samples at rows[c * rs ..], rs = bsmax + 32 */
-    const uint32_t lane = threadIdx.x & 63u, f = blockIdx.x;
-    if (f >= nframes) return;
-    const uint32_t st0 = info[f].status;
-    if (st0 != BNF_ST_OK) return;
-    bnf_frame_info fi = info[f];
-    const uint32_t C = wr_u(fi.channels), bs = wr_u(fi.blocksize);
-    const uint64_t limit = nbytes * 8u;
-    /* unsupported layouts and short buffers: SKIPPED, no decode (k_decode's rules) */
-    {
-        uint32_t fl = 0;
-        if (fmt == BNF_OUT_FLACDECODER && fi.bps != 16) fl = BNF_FL_UNSUPPORTED;
-        if (fmt >= BNF_OUT_FLACDECODER && C > sp.channels) fl = BNF_FL_UNSUPPORTED;
-        if (fmt == BNF_OUT_FILEREADER && sp.bps != 16 && sp.bps != 24) fl = BNF_FL_UNSUPPORTED;
-        uint64_t stride;
-        switch (fmt) {
-        case BNF_OUT_PLANAR32: case BNF_OUT_INTERLEAVED32: stride = 4ull * sp.channels; break;
-        case BNF_OUT_FLACDECODER: stride = C == 2 ? 4u : 2u; break;
-        default: stride = (uint64_t)sp.channels * (sp.bps == 24 ? 3u : 2u); break;
-        }
-        if (!fl && (fi.out_sample + bs) * stride > out_bytes) fl = BNF_FL_OUT_OF_BOUNDS;
-        if (!fl && C > 8u) fl = 8u; /* never for FLAC's 3-bit field: the lane kernels' SKIPPED */
-        if (fl) {
-            if (lane == 0) {
-                info[f].status = BNF_ST_SKIPPED;
-                info[f].flags = fi.flags | (fl & 6u);
-            }
-            return;
-        }
-        if (C > cmax || bs > bsmax) { /* wider than this launch's rows */
-            if (lane == 0) info[f].flags = fi.flags | BNF_FL_WAVE_REDO;
-            return;
-        }
-    }
-    const uint32_t rs = bsmax + 32u;
-    const bool tmon = (ablate & 0x100u) != 0; /* bench --stats: s_memtime per phase into g_stats[8..12] */
-    const uint64_t t0 = tnow(tmon);
-    for (uint32_t i = lane; i < 8u * 256u; i += 64u) tabs[i] = (&g_crc16_tab[0][0])[i];
-    WR r;
-    const uint64_t fbit = fi.frame_off * 8u;
-    wr_init(r, words, nbytes, (lds_u32 *)ring, fbit + fi.sub_start[0]);
-    uint32_t st = BNF_ST_OK, maxord = 0;
-    int32_t err = -1;
-    bool trunc = false;
-    for (uint32_t ch = 0; ch < C && st == BNF_ST_OK; ch++) {
-        int32_t *buf = rows + ch * rs;
-        r.pos = fbit + wr_u(info[f].sub_start[ch]); /* a record word by a run-time index: from memory, not a register array */
-        SubHdr h;
-        int32_t coef[32];
-        st = parse_subframe_head<true, 32, 1, WR>(r, sub_bps(fi, ch), bs, limit, h, buf, coef, err);
-        if (st == BNF_ST_ERROR && br_pos(r) > limit) st = BNF_ST_TRUNC;
-        if (st != BNF_ST_OK) break;
-        if (lane == 0) {
-#pragma unroll
-            for (int u = 0; u < 32; u++) ctab[ch * 32u + u] = coef[u];
-            uint32_t *ht = htab + ch * DW_TAB;
-            ht[0] = h.type;
-            ht[1] = h.order;
-            ht[2] = h.wasted;
-            ht[3] = h.path;
-            ht[4] = (uint32_t)h.shift;
-            ht[5] = (uint32_t)h.cval;
-        }
-        const uint32_t taps = h.type == T_CONST ? 1u : h.order;
-        maxord = max(maxord, taps);
-        if (h.type == T_CONST) {
-            for (uint32_t i = lane; i < bs; i += 64u) buf[i] = i ? 0 : h.cval;
-        } else if (h.type == T_VERB) {
-            wave_read_raw(r, bs, h.bps, buf);
-        } else { /* FIXED / LPC: partitioned Rice (read_residual_partitioned_rice_ @0x10012da0) */
-            const uint32_t parts = 1u << h.porder;
-            const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
-            const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
-            uint32_t idx = h.order;
-            for (uint32_t p = 0; p < parts; p++) {
-                if (br_pos(r) > limit) { trunc = true; break; }
-                const uint32_t kk = wr_u(br_read(r, plen));
-                const uint32_t cnt = (h.porder == 0 || p > 0) ? psamples : psamples - h.order;
-                if (kk >= pesc) {
-                    const uint32_t nb = wr_u(br_read(r, 5));
-                    wave_read_raw(r, cnt, nb, buf + idx);
-                } else if (cnt && !wave_rice_dec_any(r, cnt, kk, limit, buf + idx)) {
-                    trunc = true;
-                    break;
-                }
-                idx += cnt;
-            }
-        }
-        if (trunc || br_pos(r) > limit) { trunc = true; break; }
-    }
-    /* the frame's end: zero padding, CRC-16 footer (read_frame_ @0x100118c0 tail) */
-    uint32_t t_status = BNF_ST_OK, crc_read = 0;
-    uint64_t resume = 0, end_byte = 0;
-    bool resume_set = false;
-    if (st == BNF_ST_ERROR) {
-        t_status = BNF_ST_ERROR;
-        resume = br_pos(r);
-        resume_set = true;
-    } else if (st == BNF_ST_TRUNC || trunc) {
-        t_status = BNF_ST_TRUNC;
-    } else {
-        const uint32_t padbits = (uint32_t)((8u - (br_pos(r) & 7u)) & 7u);
-        const uint32_t z = br_read(r, padbits);
-        if (br_pos(r) > limit) {
-            t_status = BNF_ST_TRUNC;
-        } else if (z != 0) {
-            t_status = BNF_ST_ERROR;
-            err = E_LOST_SYNC;
-            resume = br_pos(r);
-            resume_set = true;
-        } else {
-            end_byte = br_pos(r) >> 3;
-            crc_read = br_read(r, 16);
-            if (br_pos(r) > limit) t_status = BNF_ST_TRUNC;
-            else {
-                resume = br_pos(r);
-                resume_set = true;
-            }
-        }
-    }
-    wait_vm(); /* the reader's windows have landed: the stores below are the wave's only memory ops */
-    __syncthreads();
-    const uint64_t t1 = tnow(tmon);
-    uint32_t crc = 0;
-    if (t_status == BNF_ST_OK) { /* CRC-16 of [frame_off, end_byte): 64 slices, shifted and XOR-reduced */
-        const uint64_t len = end_byte - fi.frame_off, per = (len + 63u) / 64u;
-        const uint64_t s0 = fi.frame_off + min(len, per * lane), s1 = fi.frame_off + min(len, per * (lane + 1u));
-        uint32_t part = crc16_range((const uint8_t *)words, s0, s1, (const lds_u16 *)tabs);
-        part = crc16_shift(part, end_byte - s1);
-        for (int o = 32; o > 0; o >>= 1) part ^= (uint32_t)__shfl_xor((int)part, o);
-        crc = wr_u(part);
-    }
-    const bool ok = t_status == BNF_ST_OK && crc == crc_read;
-    const uint64_t t2 = tnow(tmon);
-    uint64_t t3 = t2;
-    if (t_status == BNF_ST_OK) { /* restore: lane ch < C, its channel's rows in place */
-        DwHdr h;
-        const uint32_t ch = min(lane, C - 1u);
-        const uint32_t *ht = htab + ch * DW_TAB;
-        h.type = ht[0];
-        h.order = ht[1];
-        h.wasted = ht[2];
-        h.path = ht[3];
-        h.shift = (int32_t)ht[4];
-        h.cval = (int32_t)ht[5];
-        if (lane < C) {
-            int32_t *buf = rows + lane * rs;
-            if (maxord <= 8u) dw_restore<8>(buf, bs, ctab + lane * 32u, h);
-            else if (maxord <= 16u) dw_restore<16>(buf, bs, ctab + lane * 32u, h);
-            else dw_restore<32>(buf, bs, ctab + lane * 32u, h);
-        }
-        __syncthreads();
-        t3 = tnow(tmon);
-        /* decorrelation and the output layout; a CRC failure writes zeros (@0x10011af5) */
-        const uint32_t as = fi.assignment, sc = sp.channels;
-        const uint64_t os = fi.out_sample;
-        for (uint32_t n = lane; n < bs; n += 64u) {
-            int32_t v[8];
-#pragma unroll
-            for (int c = 0; c < 8; c++) v[c] = ((uint32_t)c < C && ok) ? rows[c * rs + n] : 0;
-            if (C == 2u && ok) decorrelate(as, v[0], v[1]);
-            switch (fmt) {
-            case BNF_OUT_PLANAR32: {
-                int32_t *o = (int32_t *)out + os * sc;
-#pragma unroll
-                for (int c = 0; c < 8; c++)
-                    if ((uint32_t)c < C) o[(uint64_t)c * bs + n] = v[c];
-                break;
-            }
-            case BNF_OUT_INTERLEAVED32: {
-                int32_t *o = (int32_t *)out + (os + n) * sc;
-#pragma unroll
-                for (int c = 0; c < 8; c++)
-                    if ((uint32_t)c < C) o[c] = v[c];
-                break;
-            }
-            case BNF_OUT_FLACDECODER: /* FLACDecoder.cs:543-577 */
-                if (C == 2u) ((uint32_t *)out)[os + n] = ((uint32_t)v[0] & 0xffffu) | ((uint32_t)v[1] << 16);
-                else ((uint16_t *)out)[os + n] = (uint16_t)(uint32_t)v[0];
-                break;
-            default: { /* FLACFileReader.cs:220-237 */
-                const uint32_t fb = sp.bps == 24 ? 3u : 2u;
-                uint8_t *o = out + (os + n) * (uint64_t)sc * fb;
-#pragma unroll
-                for (int c = 0; c < 8; c++)
-                    if ((uint32_t)c < C) {
-                        o[c * fb] = (uint8_t)v[c];
-                        o[c * fb + 1] = (uint8_t)(v[c] >> 8);
-                        if (fb == 3) o[c * fb + 2] = (uint8_t)(v[c] >> 16);
-                    }
-                break;
-            }
-            }
-        }
-    }
-    if (tmon && lane == 0) { /* decode (headers + Rice), CRC, restore, pack */
-        const uint64_t t4 = tnow(tmon);
-        atomicAdd(&g_stats[8], (unsigned long long)(t1 - t0));
-        atomicAdd(&g_stats[9], (unsigned long long)(t2 - t1));
-        atomicAdd(&g_stats[10], (unsigned long long)(t3 - t2));
-        atomicAdd(&g_stats[11], (unsigned long long)(t4 - t3));
-        atomicAdd(&g_stats[5], 1ull);
-    }
-    if (lane == 0) { /* the record: every word but crc_next (k_decode's write) */
-        bnf_frame_info fo = fi;
-        fo.status = t_status;
-        if (t_status == BNF_ST_ERROR) fo.err = err;
-        if (resume_set) fo.resume_bit = resume;
-        if (t_status == BNF_ST_OK) {
-            fo.crc16_read = crc_read;
-            fo.crc16_calc = crc;
-            fo.crc_ok = ok ? 1u : 0u;
-        }
-        const uint32_t *src = (const uint32_t *)&fo;
-        uint32_t *dst = (uint32_t *)&info[f];
-#pragma unroll
-        for (int i = 0; i < 31; i++) dst[i] = src[i];
-    }
-}
-
-extern "C" {
-hipError_t TU_FN(bnf_upload_tables)(const uint8_t *crc8, const uint16_t *crc16x8, const uint16_t *xpow) {
-    return upload_tables(crc8, crc16x8, xpow);
-}
-/* rows for cmax channels of bsmax samples; false when they do not fit the LDS */
-size_t bnf_decode_wave_lds(uint32_t cmax, uint32_t bsmax) { return (size_t)cmax * (bsmax + 32u) * 4u; }
-hipError_t TU_FN(bnf_launch_decode_wave)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
-                                         int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info, uint32_t cmax,
-                                         uint32_t bsmax, hipStream_t s) {
-    /* the dynamic-LDS limit is a per-device function attribute: set once for each device */
-    static std::atomic<uint8_t> attr_set[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    if (!attr_set[dev].load(std::memory_order_acquire)) {
-        const hipError_t attr = hipFuncSetAttribute((const void *)k_decode_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    (160 << 10) - (int)(14u << 10)); /* rows above 64 KB */
-        if (attr != hipSuccess) return attr;
-        attr_set[dev].store(1, std::memory_order_release);
-    }
-    hipLaunchKernelGGL(k_decode_wave, dim3(nframes), dim3(64), bnf_decode_wave_lds(cmax, bsmax), s, words, nbytes, nframes,
-                       sp, fmt, out, out_bytes, info, cmax, bsmax, ablate_flags());
-    return hipGetLastError();
-}
-void TU_FN(bnf_set_ablate)(uint32_t v) { g_ablate.store(v, std::memory_order_relaxed); }
-hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
-    uint64_t v[16];
-    hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stats), sizeof v);
-    if (e != hipSuccess) return e;
-    for (int i = 0; i < 16; i++) out16[i] += v[i];
-    if (reset) {
-        static const uint64_t z[16] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z);
-    }
-    return e;
-}
-} /* extern "C" */
-#endif
-
 #if BNF_TU == 0
 extern "C" {
 hipError_t bnf_upload_tables_tu3(const uint8_t *, const uint16_t *, const uint16_t *);
@@ -4711,13 +4322,9 @@ hipError_t bnf_launch_decode_tu5(const uint32_t *, uint64_t, uint32_t, bnf_strea
                                  uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, const uint32_t *, hipStream_t);
 hipError_t bnf_upload_tables_tu1(const uint8_t *, const uint16_t *, const uint16_t *);
 hipError_t bnf_upload_tables_tu2(const uint8_t *, const uint16_t *, const uint16_t *);
-hipError_t bnf_upload_tables_tu6(const uint8_t *, const uint16_t *, const uint16_t *);
-void bnf_set_ablate_tu6(uint32_t);
-hipError_t bnf_stats_tu6(uint64_t *, int);
 hipError_t bnf_upload_tables_tu7(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu7(uint32_t);
 hipError_t bnf_stats_tu7(uint64_t *, int);
-size_t bnf_decode_wave_lds(uint32_t, uint32_t);
 hipError_t bnf_upload_tables_tu8(const uint8_t *, const uint16_t *, const uint16_t *);
 hipError_t bnf_stats_tu8(uint64_t *, int);
 void bnf_set_ablate_tu8(uint32_t);
@@ -4725,8 +4332,6 @@ hipError_t bnf_launch_decode_sys_tu8(const uint32_t *, uint64_t, uint32_t, bnf_s
                                      uint64_t, bnf_frame_info *, const uint32_t *, uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_launch_decode_list_tu2(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
                                       uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
-hipError_t bnf_launch_decode_wave_tu6(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, int, uint8_t *, uint64_t,
-                                      bnf_frame_info *, uint32_t, uint32_t, hipStream_t);
 void bnf_set_ablate_tu1(uint32_t);
 void bnf_set_ablate_tu2(uint32_t);
 hipError_t bnf_stats_tu1(uint64_t *, int);
@@ -4743,7 +4348,6 @@ hipError_t bnf_upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, const
     if (e == hipSuccess) e = bnf_upload_tables_tu3(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu4(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu5(crc8, crc16x8, xpow);
-    if (e == hipSuccess) e = bnf_upload_tables_tu6(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu7(crc8, crc16x8, xpow);
     if (e == hipSuccess) e = bnf_upload_tables_tu8(crc8, crc16x8, xpow);
     return e;
@@ -4772,7 +4376,6 @@ void bnf_set_ablate(uint32_t v) {
     bnf_set_ablate_tu3(v);
     bnf_set_ablate_tu4(v);
     bnf_set_ablate_tu5(v);
-    bnf_set_ablate_tu6(v);
     bnf_set_ablate_tu7(v);
     bnf_set_ablate_tu8(v);
 }
@@ -4783,7 +4386,6 @@ hipError_t bnf_stats(uint64_t *out16, int reset) {
     if (e == hipSuccess) e = bnf_stats_tu2(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu3(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu5(out16, reset);
-    if (e == hipSuccess) e = bnf_stats_tu6(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu7(out16, reset);
     if (e == hipSuccess) e = bnf_stats_tu8(out16, reset);
     return e == hipSuccess ? bnf_stats_tu4(out16, reset) : e;
@@ -4946,35 +4548,6 @@ static bool use_parse_wave(uint32_t nframes, const bnf_stream_params &sp) {
     return nframes <= 8192u || (nframes <= 32768u && (sp.bps > 16u || sp.channels > 2u));
 }
 
-/* Decode kernel choice: k_decode_wave when the batch is too small for lane-per-frame waves to
- * fill the chip and its frames' rows fit one workgroup's LDS (STREAMINFO's max blocksize x the
- * channel lanes).  BNFLAC_DECODE_WAVE=0 never, 1 whenever the rows fit; default: up to two
- * workgroups per LDS slot of the device (see bnflac_decode_wave_lds and DESIGN.md). */
-#ifndef DW_AUTO
-#define DW_AUTO 0 /* auto mode off until k_decode_wave beats the lane kernels on small batches */
-#endif
-static std::atomic<int> g_decode_wave{-1};
-static bool use_decode_wave(uint32_t nframes, uint32_t cmax, uint32_t bsmax) {
-    int m = g_decode_wave.load(std::memory_order_relaxed);
-    if (m < 0) {
-        const char *e = getenv("BNFLAC_DECODE_WAVE");
-        m = e ? (atoi(e) ? 1 : 0) : 2;
-        g_decode_wave.store(m, std::memory_order_relaxed);
-    }
-    if (!m || !bsmax || !cmax || cmax > 8u) return false;
-    const size_t lds = bnf_decode_wave_lds(cmax, bsmax), fixed = 14u << 10;
-    if (lds + fixed > (160u << 10)) return false;
-    if (m == 1) return true;
-    static const uint32_t cus = [] {
-        int d = 0, cu = 256;
-        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-            cu = 256;
-        return (uint32_t)std::max(cu, 1);
-    }();
-    const uint32_t wpc = std::min<uint32_t>(8u, (uint32_t)((160u << 10) / (lds + fixed)));
-    return DW_AUTO && nframes <= 2u * cus * wpc;
-}
-
 /* k_decode_sys (systolic restore, every frame class) or the lane kernels by class.  The lane
  * kernels run one subframe per lane (k_decode_st: one stereo frame), so a launch of few frames is
  * a few waves, each as long as one lane's serial chain; k_decode_sys spreads each subframe over a
@@ -4995,7 +4568,6 @@ static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32
     (void)sp;
     if (chn_lanes > 8u || m == 0) return false;
     if (m == 1) return true;
-    if (g_decode_wave.load(std::memory_order_relaxed) == 1) return false; /* k_decode_wave forced */
     static const uint32_t lim = [] {
         const char *e = getenv("BNFLAC_SYS_WAVES");
         return e ? (uint32_t)strtoul(e, nullptr, 0) : SYS_AUTO_WAVES;
@@ -5005,7 +4577,6 @@ static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32
 
 extern "C" {
 void bnf_set_decode_sys(int mode) { g_decode_sys.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
-void bnf_set_decode_wave(int mode) { g_decode_wave.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
 void bnf_set_parse_wave(int mode) { g_parse_wave.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
 hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset) { /* debug counters of k_parse_wave (BNFLAC_PW_STATS=1) */
     hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_pw_stats), 8 * sizeof(uint64_t));
@@ -5066,17 +4637,6 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         if (e == hipSuccess)
             e = bnf_launch_decode_list_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, list, mode, s);
         return e;
-    }
-    /* small launches: a wave per frame (k_decode_wave), then the lane kernels for its
-     * hand-backs only (frames wider than STREAMINFO's bounds) */
-    {
-        const uint32_t cmax = chn_lanes, bsmax = sp.has_stream_info ? sp.max_blocksize : 0u;
-        if (use_decode_wave(nframes, cmax, bsmax)) {
-            hipError_t e = bnf_launch_decode_wave_tu6(words, nbytes, nframes, sp, fmt, out, out_bytes, info, cmax, bsmax, s);
-            if (e != hipSuccess) return e;
-            mode |= BNF_MODE_WREDO;
-            order = nullptr; /* no class order: every lane-kernel block leaves unless it holds a hand-back */
-        }
     }
     const uint32_t *perm = nullptr;
     if (order) {

@@ -152,9 +152,6 @@ extern "C" BNFLAC_API void bnflac_debug_set_crc_pass(int on) { g_crc_pass = std:
 extern "C" void bnf_set_parse_wave(int mode);
 /* parse kernel: -1 auto (k_parse_wave for small launches), 0 k_parse, 1 k_parse_wave (tests, A/B) */
 extern "C" BNFLAC_API void bnflac_debug_set_parse_wave(int mode) { bnf_set_parse_wave(mode); }
-extern "C" void bnf_set_decode_wave(int mode);
-/* k_decode_wave: -1 auto (DW_AUTO: currently never), 0 off, 1 whenever the rows fit (tests, A/B) */
-extern "C" BNFLAC_API void bnflac_debug_set_decode_wave(int mode) { bnf_set_decode_wave(mode); }
 extern "C" void bnf_set_decode_sys(int mode);
 /* k_decode_sys (systolic restore, every frame class): -1 auto (BNFLAC_DECODE_SYS), 0 the lane
  * kernels by class, 1 always (tests, A/B) */

@@ -190,13 +190,9 @@ BNFLAC_API void bnflac_debug_set_crc_pass(int on);
 /* Development / test switch: parse kernel (-1 auto, 0 lane-per-frame k_parse, 1 wave-per-frame
  * k_parse_wave); both write identical records. */
 BNFLAC_API void bnflac_debug_set_parse_wave(int mode);
-/* Development / test switch: decode kernels (-1 auto -- currently never, 0 the lane kernels
- * k_decode_st / k_decode<W>, 1 the wave-per-frame k_decode_wave whenever STREAMINFO's bounds fit
- * its rows); the PCM and records of every decoded frame are identical. */
-BNFLAC_API void bnflac_debug_set_decode_wave(int mode);
 /* Development / test switch: k_decode_sys, the systolic-restore decode of every frame class
- * (-1 auto: env BNFLAC_DECODE_SYS, 0 the lane kernels by class, 1 always); identical PCM and
- * records. */
+ * (-1 auto: env BNFLAC_DECODE_SYS, else k_decode_sys for launches below 1024 subframe waves of
+ * the lane kernels; 0 the lane kernels by class; 1 always); identical PCM and records. */
 BNFLAC_API void bnflac_debug_set_decode_sys(int mode);
 /* Debug: k_parse_wave's counters, collected while BNFLAC_PW_STATS is set in the environment
  * (passes, splice rounds, serial fallbacks, partitions, frames, scan / window-wait / splice

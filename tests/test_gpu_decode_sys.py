@@ -157,6 +157,20 @@ def test_lpc_restore_paths(gpu, order, prec, stereo):
     assert np.array_equal(pcm, oracle.interleave(ev, opcm))
 
 
+@pytest.mark.parametrize("order,stereo", [(2, 3), (4, 1), (3, 0)])
+def test_fixed_24bit_side_leaves_24_bits(gpu, order, stereo):
+    """FIXED subframes of 24-bit stereo (the side channel has 25 bits, its FIXED sums wrap in
+    32 bits): identical to the lane kernels and the generator's PCM."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _, _ = gpu
+    s = synth.encode(synth.config("C3", nframes=6, last_blocksize=0, subframe_mode=synth.SUB_FIXED, order=order,
+                                  stereo_mode=stereo, level=0.95, noise=0.3, wasted_bits_max=0, seed=40 + order))
+    data = s.data.tobytes()
+    assert _same(gpu, data, _offsets(s), libflac.OUT_INTERLEAVED32)[0] == 6
+    _, out, _ = _decode(gpu, data, _offsets(s), libflac.OUT_INTERLEAVED32, True, _sp(libflac, data))
+    assert np.array_equal(out[:s.nsamples * 8].view("<i4").reshape(-1, 2), s.pcm)
+
+
 def test_damaged_and_truncated_identical(gpu):
     """Byte flips (CRC failures, damaged residuals and headers) and cut streams: same records,
     same PCM for every frame that decodes, CRC-failed frames zero-filled."""

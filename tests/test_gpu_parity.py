@@ -39,14 +39,12 @@ def gpu():
 @pytest.fixture
 def decode_mode(request, gpu):
     """The decode kernels for one test: 0 the lane kernels (k_decode_st / k_decode_sw /
-    k_decode<W>), 1 the wave-per-frame k_decode_wave, 2 k_decode_sys (systolic restore, every
-    frame class; its hand-backs through k_decode_list).  Auto (-1 on both switches) afterwards."""
+    k_decode<W>), 2 k_decode_sys (systolic restore, every frame class; its hand-backs through
+    k_decode_list).  Auto (-1) afterwards."""
     torch, libflac, _ = gpu
     L = libflac.load()
-    L.bnflac_debug_set_decode_wave(1 if request.param == 1 else 0)
     L.bnflac_debug_set_decode_sys(1 if request.param == 2 else 0)
     yield request.param
-    L.bnflac_debug_set_decode_wave(-1)
     L.bnflac_debug_set_decode_sys(-1)
 
 
@@ -120,7 +118,7 @@ def test_rfc9639_example2_frame1_gpu(gpu):
     assert _sha(pcm) == g["pcm_sha256_oracle"]
 
 
-@pytest.mark.parametrize("decode_mode", [0, 1, 2], indirect=True)
+@pytest.mark.parametrize("decode_mode", [0, 2], indirect=True)
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
 def test_config_batch_vs_oracle_and_source(gpu, cfg, decode_mode):
     import oracle
@@ -139,7 +137,7 @@ def test_config_batch_vs_oracle_and_source(gpu, cfg, decode_mode):
 
 @pytest.mark.parametrize("order,prec,stereo", [(2, 15, 0), (3, 0, 3), (4, 12, 0), (8, 15, 1), (8, 0, 2),
                                                 (12, 15, 3), (16, 0, 0), (32, 15, 3), (32, 0, 0)])
-@pytest.mark.parametrize("decode_mode", [0, 1, 2], indirect=True)
+@pytest.mark.parametrize("decode_mode", [0, 2], indirect=True)
 def test_lpc_restore_paths_16bit(gpu, order, prec, stereo, decode_mode):
     """Every libFLAC restore path on 16-bit input (MMX for order >= 4 at <= 32 bits, ia32
     for low orders, the 64-bit path when bps + precision + log2(order) > 32 -- no encoder
