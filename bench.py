@@ -555,7 +555,7 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank, files=None,
     concurrent RCCL receives over xGMI)."""
     from birdnest.audio_amd import shard
     F = files or args.batches or CONFIGS["C5"]["batches"]
-    steps = steps or steps
+    steps = steps or args.steps
     warmup = args.warmup if warmup is None else warmup
     p0 = synth.config("C5")
     ranges = shard.partition([p0.nframes * p0.blocksize] * F, world)  # equal files: F/world each
@@ -686,7 +686,7 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank, files=None,
 def c5_summary(r, args, world, steps=None):
     """value / timing / roofline fields of a c5_job result (the --config C5 line, the C5 leg at
     N = 1, or the C5 flow leg of a multi-GPU C2 run)."""
-    steps = steps or steps
+    steps = steps or args.steps
     step_ms = r["t_dec"] / steps * 1e3
     out = {"value": round(r["samples"] * steps / r["t_dec"] / 1e6, 2), "unit": "MSamples/s",
            "ms_per_step": round(step_ms, 4), "bitexact": r["ok"], "files": r["files"], "ranks": world,

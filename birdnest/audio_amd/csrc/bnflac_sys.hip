@@ -52,11 +52,20 @@
 #define SYS_RP 80                    /* row stride (dwords), [sample][slot]: 80 = 16 mod 64 banks */
 #define SYS_CW 4                     /* restore waves per workgroup (16 subframe slots each) */
 #define SYS_THREADS (64 * (1 + SYS_CW))
-#define SYS_RD 16                    /* producer ring: 16-byte blocks per lane (256 B ahead of the cursor) */
+/* ring refills by the restore waves (1) or by the producer (0): see the producer's chunk loop */
+#ifndef SYS_HELPERS
+#define SYS_HELPERS 0
+#endif
+#ifndef SYS_RD                       /* producer ring: 16-byte blocks per lane */
+#define SYS_RD (SYS_HELPERS ? 32 : 16)
+#endif
 #define SYS_HALF 16                  /* producer step: residuals per refill and per fast run */
 #define SYS_CS 33                    /* coefficient table stride per slot (bank spread) */
+#define SYS_HB 2                     /* ring blocks each restore wave loads per producer lane and chunk */
 
 static_assert(SYS_CHK == 32, "the restore chunk is written for 32 samples (8 per quad lane)");
+static_assert(SYS_HB == 2, "the helpers' in-flight test is written for two blocks");
+DEV bool sys_helpers(uint32_t ablate) { return SYS_HELPERS == 1 || (SYS_HELPERS == 2 && !(ablate & 0x2000000u)); }
 static_assert(64 * SYS_CS * 4 <= SYS_CHK * SYS_RP * 4, "the coefficient table overlays row buffer 1");
 static_assert((8 * 256 + 512) * 2 <= SYS_CHK * SYS_RP * 4, "the CRC tables overlay row buffer 0");
 
@@ -71,6 +80,7 @@ enum { FS_NONE = 0, FS_DEC = 1, FS_TAIL = 2 };
 struct SysShared {
     uint32_t ring[SYS_RD * RING_LANE_DW];  /* producer bit rings: LDS-DMA images, 1 KiB aligned (first) */
     int32_t rows[2][SYS_CHK * SYS_RP];     /* residuals in, samples out; [1] holds the coefficients at setup */
+    uint32_t r_lo[2][64], r_hi[2][64];     /* the producer's ring requests by chunk parity: blocks [lo, hi) per lane */
     uint32_t p_order[64], p_sh[64], p_flags[64], p_wasted[64], p_bs[64];
     uint32_t f_idx[64], f_bs[64], f_ch[64], f_as[64], f_state[64], f_end[64], f_crc[64], f_bad[64];
     uint64_t f_os[64], f_off[64], f_resume[64];
@@ -78,37 +88,44 @@ struct SysShared {
 };
 
 DEV void sys_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-/* debug phase timers (ablate 0x100, bench.py --stats): s_memtime, wave-uniform points only */
-DEV uint64_t sys_now(bool on) {
-    if (!on) return 0ull;
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    return t;
-}
+/* debug phase timers (ablate 0x100, bench.py --stats): s_memtime, wave-uniform points only.
+ * Compiled in only with -DBNFLAC_PHASE_TIMERS (a variant build, tools/sys_stats.sh): a scalar-
+ * memory op anywhere in the producer loop makes hipcc's LDS waits lgkmcnt(0) (the ring lookahead
+ * reads then wait at every step instead of 1.5 steps later). */
+DEV uint64_t sys_now(bool on) { return tnow(on); }
 
-/* 4-deep producer refill, every SYS_HALF residuals: the DMAs of the last three refills may stay
+/* Producer refill, pipelined RQ deep: at refill r the DMAs of refills r - 1 .. r - RQ may stay
  * in flight (vmcnt retires in issue order and the producer issues no other vector-memory ops),
  * everything issued before them has landed.  Then the blocks up to SYS_RD past the cursor's
- * block.  d*: DMA instructions of the last refills (wave-uniform), e*: the lane's iend when
- * each of them started (shift registers, so every index is a compile-time constant). */
+ * block, one exec-masked DMA per ring slot (each slot's LDS base is wave-uniform; lane l's block
+ * j lands in slot j mod SYS_RD).  d[i]: DMA instructions of refill r - 1 - i (wave-uniform),
+ * e[i]: the lane's iend after refill r - 1 - i (shift registers: compile-time indices).
+ * Called every SYS_HALF residuals with RQ = 3, or once per chunk with RQ = 1 (ablate 0x1000000:
+ * half the DMA instructions per residual, one chunk of latency cover). */
+#define SYS_RQMAX 3
 struct SysQ {
-    uint32_t d0, d1, d2;
-    uint32_t e0, e1, e2;
+    uint32_t d[SYS_RQMAX];
+    uint32_t e[SYS_RQMAX + 1];
     uint64_t tw, dw; /* stats mode: wait cycles, DMA instructions waited past (flushed once per wave) */
 };
 __device__ unsigned long long g_sys_dbg[4]; /* debug: refill wait cycles, DMA instructions (stats mode) */
+template <int RQ>
 DEV void sys_refill(BR &b, bool want, SysQ &q, bool tm = false) {
-    const uint64_t tw = tm ? __builtin_amdgcn_s_memtime() : 0ull;
-    wait_vm_n(q.d0 + q.d1 + q.d2);
+    static_assert(RQ >= 1 && RQ <= SYS_RQMAX, "refill depth");
+    const uint64_t tw = tnow(tm);
+    uint32_t fly = 0;
+#pragma unroll
+    for (int i = 0; i < RQ; i++) fly += q.d[i];
+    wait_vm_n(fly);
+#ifdef BNFLAC_PHASE_TIMERS
     if (tm) { /* no global atomics here: their vmcnt wait would drain the DMAs in flight */
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        q.tw += __builtin_amdgcn_s_memtime() - tw;
-        q.dw += q.d0 + q.d1 + q.d2;
+        q.tw += tnow(tm) - tw;
+        q.dw += fly;
     }
-    b.vendw = max(b.vendw, q.e2 * 4u); /* issued before the refill three back: landed */
-    q.e2 = q.e1;
-    q.e1 = q.e0;
-    q.e0 = b.iend;
+#else
+    (void)tw;
+#endif
+    b.vendw = max(b.vendw, q.e[RQ] * 4u); /* issued by refill r - 1 - RQ or earlier: landed */
     const uint32_t cb = b.wi >> 2;
     const uint32_t lo = max(b.iend, cb), hi = cb + b.rdepth;
     uint32_t d = 0;
@@ -122,16 +139,21 @@ DEV void sys_refill(BR &b, bool want, SysQ &q, bool tm = false) {
         }
     }
     if (want) b.iend = max(b.iend, hi);
-    q.d2 = q.d1;
-    q.d1 = q.d0;
-    q.d0 = d;
+#pragma unroll
+    for (int i = SYS_RQMAX - 1; i > 0; i--) q.d[i] = q.d[i - 1];
+    q.d[0] = d;
+#pragma unroll
+    for (int i = SYS_RQMAX; i > 0; i--) q.e[i] = q.e[i - 1];
+    q.e[0] = b.iend;
 }
 
 /* ------------------------------------------------------------------ producer fast path */
-/* Ring byte address of word wi (bits 2-3 word in block, 4-9 lane, 10-13 slot), moved on one word
- * by ((ra | 0x3F3) + c) & 0x3C0C | lane bits (k_decode_st's incremental form, 16 slots) */
-static_assert(SYS_RD == 16, "sys_adv's address arithmetic is written for 16 ring slots");
-DEV uint32_t sys_ra(uint32_t wi, uint32_t lane) { return ((wi & 3u) << 2) | (lane << 4) | (((wi >> 2) & 15u) << 10); }
+/* Ring byte address of word wi (bits 2-3 word in block, 4-9 lane, 10 and up slot), moved on one
+ * word by ((ra | 0x3F3) + c) & SYS_RAM | lane bits (k_decode_st's incremental form): the ones in
+ * bits 0-1 turn +c into +4, the ones in bits 4-9 carry a block wrap into the slot */
+static_assert((SYS_RD & (SYS_RD - 1)) == 0 && SYS_RD <= 32, "ring slots: a power of two");
+#define SYS_RAM (0xCu | ((SYS_RD - 1u) << 10))
+DEV uint32_t sys_ra(uint32_t wi, uint32_t lane) { return ((wi & 3u) << 2) | (lane << 4) | (((wi >> 2) & (SYS_RD - 1u)) << 10); }
 DEV void sys_adv(BR &b, uint32_t n, uint32_t laneb) { /* n <= 32, no landing check */
     uint32_t t;
     const bool c = __builtin_usub_overflow(b.s, n, &t);
@@ -139,148 +161,22 @@ DEV void sys_adv(BR &b, uint32_t n, uint32_t laneb) { /* n <= 32, no landing che
     b.hi = c ? b.lo : b.hi;
     b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
     b.wi += (uint32_t)c;
-    b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x3C0Cu) | laneb;
+    b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & SYS_RAM) | laneb;
 }
 DEV void sys_next_word(BR &b) { b.nx = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + b.ra); }
 DEV void sys_resync(BR &b, uint32_t lane) { b.ra = sys_ra(b.wi, lane); b.vlim = b.vendw - 1u; }
 DEV int32_t sys_zz(uint32_t u) { return (int32_t)((u >> 1) ^ (0u - (u & 1u))); }
-/* rare cases of a fast step: the cursor entered ring words not known to have landed (wait for
- * every DMA, refill if still short, read the word again), or a codeword / pair too long for the
- * window (this lane did not advance: decode it with the generic reader) */
-template <int NW>
-DEV void sys_rare(BR &b, bool sl, bool ld, uint32_t k, uint32_t (&u)[NW], uint64_t limit, uint32_t &trunc, uint32_t lane) {
-    if (any_lane(ld)) {
-        STAT(b.stats, 2);
-        wait_vm();
-        b.vendw = b.iend * 4u;
-        if (b.wi + 1u >= b.vendw) {
-            br_refill(b);
-            wait_vm();
-            br_drained(b);
-        }
-        sys_resync(b, lane);
-        sys_next_word(b);
-    }
-    if (any_lane(sl)) {
-        STAT(b.stats, 3);
-        if (sl) {
-#pragma unroll
-            for (int i = 0; i < NW; i++) {
-                uint32_t qq;
-                if (!br_unary(b, qq, limit)) trunc = 1;
-                u[i] = (qq << k) | br_read(b, k);
-            }
-        }
-        sys_resync(b, lane);
-    }
-}
-/* SYS_HALF Rice codewords of one partition (parameter k; km = 31 - k, k1 = k + 1, k32 = 32 - k),
- * unchecked except for a landing test per step, into registers.  PAIR: two codewords per 32-bit
- * window (small k: C2's ~10-bit codewords) with one advance.  A step moves the window by at most
- * one word, so the word entering it at step T + 2 is the one after the window's at step T + 1 or
- * the one after that: the ring read of the latter is issued at the end of step T and selected at
- * step T + 2 (nw = c ? z : nw), a step and a half after its issue -- the LDS latency is off the
- * cursor chain, which the single-read-per-advance form (br_adv) waits for every step. */
-template <bool PAIR>
-DEV void sys_rice_run(BR &b, bool on, uint32_t k, uint32_t km, uint32_t k1, uint32_t k32, int32_t (&r)[SYS_HALF],
-                      uint64_t limit, uint32_t &trunc, uint32_t lane) { /* on: this lane decodes (others stand still) */
-    const uint32_t laneb = lane << 4;
-    sys_resync(b, lane);
-    /* nw: ring[wi] at this step (the word entering at a crossing); z1 / z2: ring[wi + 1] as issued
-     * at the end of the last step / the one before; cprev: the last step crossed.  Then
-     * nw(T) = c(T-1) ? z(T-2) : nw(T-1) -- z(T-2) was issued a step and a half earlier. */
-    if (__builtin_expect(any_lane(on && b.wi + 1u >= b.vendw), 0)) {
-        wait_vm();
-        b.vendw = b.iend * 4u;
-        if (b.wi + 1u >= b.vendw) {
-            br_refill(b);
-            wait_vm();
-            br_drained(b);
-        }
-        sys_resync(b, lane);
-        sys_next_word(b);
-    }
-    uint32_t nw = b.nx, cprev = 0, z2 = 0, z1;
-    {
-        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & 0x3C0Cu) | laneb;
-        z1 = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + ra1);
-    }
-#pragma unroll
-    for (int T = 0; T < SYS_HALF; T += PAIR ? 2 : 1) {
-        nw = cprev ? z2 : nw;
-        const uint32_t w = br_peek(b);
-        uint32_t u[2], n;
-        bool sl;
-        if (PAIR) {
-            const uint32_t qa = min(ffbh(w), 32u);
-            const uint32_t la = qa + k1;
-            const uint32_t w2 = w << (la & 31u);
-            const uint32_t qb = min(ffbh(w2), 32u);
-            u[0] = (qa << k) | __builtin_amdgcn_ubfe(w, km - qa, k);
-            u[1] = (qb << k) | __builtin_amdgcn_ubfe(w2, km - qb, k);
-            n = la + qb + k1;
-            sl = on && n > 32u;
-        } else {
-            const uint32_t q = ffbh(w); /* ~0u for an empty window: slow */
-            u[0] = (q << k) | __builtin_amdgcn_ubfe(w, km - q, k);
-            n = q + k1;
-            sl = on && q >= k32;
-        }
-        /* advance (the window crosses at most one word) */
-        uint32_t t;
-        bool c = __builtin_usub_overflow(b.s, (sl || !on) ? 0u : n, &t);
-        b.s = t & 31u;
-        b.hi = c ? b.lo : b.hi;
-        b.lo = c ? __builtin_bswap32(nw) : b.lo;
-        b.wi += (uint32_t)c;
-        b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x3C0Cu) | laneb;
-        const bool ld = on && b.wi + 1u >= b.vendw; /* the read below must hit landed words */
-        if (__builtin_expect(any_lane(sl || ld), 0)) {
-            b.nx = c ? z1 : nw; /* the generic reader's ring[wi] */
-            if (any_lane(ld)) {
-                STAT(b.stats, 2);
-                wait_vm();
-                b.vendw = b.iend * 4u;
-                if (b.wi + 1u >= b.vendw) {
-                    br_refill(b);
-                    wait_vm();
-                    br_drained(b);
-                }
-                sys_resync(b, lane);
-                sys_next_word(b);
-            }
-            if (any_lane(sl)) {
-                STAT(b.stats, 3);
-                if (sl) {
-#pragma unroll
-                    for (int i = 0; i < (PAIR ? 2 : 1); i++) {
-                        uint32_t qq;
-                        if (!br_unary(b, qq, limit)) trunc = 1;
-                        u[i] = (qq << k) | br_read(b, k);
-                    }
-                }
-                sys_resync(b, lane);
-            }
-            nw = b.nx; /* ring[wi]: the next step reads it as nw(T + 1) */
-            c = false;
-        }
-        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & 0x3C0Cu) | laneb;
-        const uint32_t zn = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + ra1);
-        z2 = z1;
-        z1 = zn;
-        cprev = c;
-        r[T] = sys_zz(u[0]);
-        if (PAIR) r[T + 1] = sys_zz(u[1]);
-    }
-    b.nx = cprev ? z2 : nw; /* the generic reader's ring[wi] */
-}
-
-/* The same run as one straight line (no branch inside, so the compiler can count the LDS reads in
- * flight instead of draining them at every merge): the caller has made sure every word the run
- * can reach has landed (wi + 2 + SYS_HALF words), each residual is written to the lane's row as
- * it is decoded, and a lane whose codeword (pair) does not fit the 32-bit window freezes its
- * cursor there.  Returns the codewords decoded (SYS_HALF unless frozen); the caller finishes a
- * frozen lane's run with the generic reader. */
+/* SYS_HALF Rice codewords of one partition (parameter k; km = 31 - k, k1 = k + 1, k32 = 32 - k) as
+ * one straight line.  PAIR: two codewords per 32-bit window (small k: C2's ~10-bit codewords) with
+ * one advance.  A step moves the window by at most one word, so the word entering it at step
+ * T + 2 is the one after the window's at step T + 1 or the one after that: the ring read of the
+ * latter is issued at the end of step T and selected at step T + 2 (nw = c ? z : nw), a step and
+ * a half after its issue -- the LDS latency is off the cursor chain.  No branch inside, so the
+ * compiler counts the reads in flight (lgkmcnt(1..3)) instead of draining them at every merge.
+ * The caller has made sure every word the run can reach has landed (wi + 2 + SYS_HALF words);
+ * each residual goes to the lane's row as it is decoded, and a lane whose codeword (pair) does
+ * not fit the window freezes its cursor there.  Returns the codewords decoded (SYS_HALF unless
+ * frozen); the caller finishes a frozen lane's run with the generic reader. */
 template <bool PAIR>
 DEV uint32_t sys_rice_line(BR &b, bool on, uint32_t k, uint32_t km, uint32_t k1, uint32_t k32, int32_t *row,
                            uint32_t lane) {
@@ -289,7 +185,7 @@ DEV uint32_t sys_rice_line(BR &b, bool on, uint32_t k, uint32_t km, uint32_t k1,
     uint32_t nw = b.nx, cprev = 0, z2 = 0, z1, cnt = 0;
     bool frozen = !on;
     {
-        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & 0x3C0Cu) | laneb;
+        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & SYS_RAM) | laneb;
         z1 = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + ra1);
     }
 #pragma unroll
@@ -320,8 +216,8 @@ DEV uint32_t sys_rice_line(BR &b, bool on, uint32_t k, uint32_t km, uint32_t k1,
         b.hi = c ? b.lo : b.hi;
         b.lo = c ? __builtin_bswap32(nw) : b.lo;
         b.wi += (uint32_t)c;
-        b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x3C0Cu) | laneb;
-        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & 0x3C0Cu) | laneb;
+        b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & SYS_RAM) | laneb;
+        const uint32_t ra1 = (((b.ra | 0x3F3u) + 1u) & SYS_RAM) | laneb;
         const uint32_t zn = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + ra1);
         z2 = z1;
         z1 = zn;
@@ -568,7 +464,7 @@ DEV void sys_pack_prep(SysPk &k, const SysShared &S, uint32_t w, uint32_t lane, 
     }
 }
 /* one chunk; false: the generic pack must run (a frame ends part-way through this chunk) */
-DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt, uint8_t *__restrict__ out) {
+DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt, uint8_t *__restrict__ out, uint32_t &nst) {
     if (!k.ok) return false;
     if (any_lane((k.pv[0] && n0 < k.bs[0] && n0 + SYS_CHK > k.bs[0]) || (k.pv[1] && n0 < k.bs[1] && n0 + SYS_CHK > k.bs[1])))
         return false;
@@ -577,6 +473,7 @@ DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt,
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         if (!any_lane(k.pv[r] && n0 < k.bs[r])) continue; /* piece 0's frame may be out while piece 1's decodes */
+        nst++; /* one store instruction below (wave-uniform) */
         if (!k.pv[r] || n0 >= k.bs[r]) continue;
         uint32_t s0 = k.s0[r], p = k.p[r];
         const uint32_t as = k.as[r];
@@ -657,7 +554,8 @@ DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt,
 /* ------------------------------------------------------------------ restore waves */
 template <int A, int PM>
 DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint32_t nchunks, int fmt,
-                     const bnf_stream_params &sp, uint8_t *__restrict__ out, uint32_t ablate) {
+                     const bnf_stream_params &sp, uint8_t *__restrict__ out, uint32_t ablate, const uint32_t *words,
+                     uint32_t nblk) {
     constexpr int P = 4 * A;
     const uint32_t g = lane >> 2, j = lane & 3u, pl = 16u * w + g;
     const uint32_t order = S.p_order[pl], flags = S.p_flags[pl], wasted = S.p_wasted[pl], bs = S.p_bs[pl];
@@ -674,12 +572,34 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
     SysPk pk;
     sys_pack_prep(pk, S, w, lane, lg, fmt, sp);
     const bool tm = (ablate & 0x100u) != 0;
+    const bool helpers = sys_helpers(ablate); /* this wave loads SYS_HB of each producer lane's ring blocks per chunk */
+    uint32_t nst = 0;                         /* store instructions of the last iteration's pack (fast pack: counted) */
+    /* ring blocks in flight: loaded after an iteration's restore steps, written into the ring at
+     * the start of the next (the pack and the barrier wait of latency cover; only the pack's
+     * stores, all younger, may then still be in flight).  Not live across the restore steps,
+     * where the VGPR count peaks (occupancy: 4 waves per SIMD hold two workgroups per CU). */
+    u32x4 hv[SYS_HB];
     uint64_t t_st = 0, t_pk = 0, t_bw = 0;
     sys_bar(); /* end of iteration 0: the producer's chunk 0 is in rows[0]; rows[1] may be overwritten */
     for (uint32_t k = 1; k <= nchunks; k++) {
         const uint64_t t0 = sys_now(tm);
         const uint32_t n0 = (k - 1u) * SYS_CHK;
         int32_t *row = S.rows[(k - 1u) & 1u];
+        /* the producer's ring request of chunk k - 2 (blocks [lo, hi) of each of its lanes), loaded
+         * by the last iteration: into the ring (lane l's block b: slot b mod SYS_RD, the LDS-DMA
+         * image layout) */
+        if (helpers && k >= 2u) {
+            const uint32_t lo = S.r_lo[k & 1u][lane], hi = S.r_hi[k & 1u][lane];
+            if (any_lane(lo + w < hi)) {
+                wait_vm_n(nst);
+#pragma unroll
+                for (int i = 0; i < SYS_HB; i++) {
+                    const uint32_t bl = lo + w + SYS_CW * (uint32_t)i;
+                    if (bl < hi) *(lds_u32x4 *)((lds_u32 *)S.ring + ((bl & (SYS_RD - 1u)) * 64u + lane) * 4u) = hv[i];
+                }
+            }
+        }
+        nst = 0;
         int32_t v[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) v[q] = row[(j + 4u * q) * SYS_RP + pl];
@@ -694,10 +614,24 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
                 if (mmx && v[q] != (int32_t)(int16_t)v[q]) range_bad = true;
             }
         }
+        /* the producer's ring request of chunk k - 1: this wave's blocks lo + w + SYS_CW i */
+        if (helpers) {
+            uint32_t lo = S.r_lo[(k - 1u) & 1u][lane];
+            const uint32_t hi = S.r_hi[(k - 1u) & 1u][lane];
+            asm volatile("" : "+v"(lo)); /* keeps the loads below the restore steps (hv live there: VGPR peak) */
+#pragma unroll
+            for (int i = 0; i < SYS_HB; i++) {
+                const uint32_t bl = lo + w + SYS_CW * (uint32_t)i;
+                if (bl < hi) hv[i] = *(const __attribute__((address_space(1))) u32x4 *)(words + (uint64_t)min(bl, nblk - 1u) * 4u);
+            }
+        }
         lds_sync();
         const uint64_t t1 = sys_now(tm);
         if (!(ablate & 2u)) {
-            if ((ablate & 0x400000u) || !sys_pack_fast(pk, row, n0, fmt, out)) sys_pack(S, row, w, lane, lg, n0, fmt, sp, out);
+            if ((ablate & 0x400000u) || !sys_pack_fast(pk, row, n0, fmt, out, nst)) {
+                sys_pack(S, row, w, lane, lg, n0, fmt, sp, out);
+                nst = 0; /* uncounted stores: the next wait takes them all */
+            }
         }
         const uint64_t t2 = sys_now(tm);
         sys_bar();
@@ -716,10 +650,11 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
 
 template <int A>
 DEV void sys_restore_pm(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint32_t nchunks, int fmt,
-                        const bnf_stream_params &sp, uint8_t *out, int pm, uint32_t ablate) {
-    if (pm == PM_WIDE) sys_restore<A, PM_WIDE>(S, w, lane, lg, nchunks, fmt, sp, out, ablate);
-    else if (pm == PM_NARROW) sys_restore<A, PM_NARROW>(S, w, lane, lg, nchunks, fmt, sp, out, ablate);
-    else sys_restore<A, PM_MIXED>(S, w, lane, lg, nchunks, fmt, sp, out, ablate);
+                        const bnf_stream_params &sp, uint8_t *out, int pm, uint32_t ablate, const uint32_t *words,
+                        uint32_t nblk) {
+    if (pm == PM_WIDE) sys_restore<A, PM_WIDE>(S, w, lane, lg, nchunks, fmt, sp, out, ablate, words, nblk);
+    else if (pm == PM_NARROW) sys_restore<A, PM_NARROW>(S, w, lane, lg, nchunks, fmt, sp, out, ablate, words, nblk);
+    else sys_restore<A, PM_MIXED>(S, w, lane, lg, nchunks, fmt, sp, out, ablate, words, nblk);
 }
 
 /* ------------------------------------------------------------------ the kernel */
@@ -821,9 +756,10 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             if (st != BNF_ST_OK) {
                 bad = true;
             } else {
-                int32_t c[32];
+                /* the coefficient table straight from the parse (a second 32-entry register copy
+                 * made this setup the kernel's VGPR peak) */
 #pragma unroll
-                for (int t = 0; t < 32; t++) c[t] = (h.type == T_LPC && (uint32_t)t < h.order) ? coef[t] : 0;
+                for (int t = 0; t < 32; t++) cf[t] = (h.type == T_LPC && (uint32_t)t < h.order) ? coef[t] : 0;
                 order = h.order;
                 if (h.type == T_LPC) {
                     if (h.path == P_WIDE) {
@@ -838,17 +774,15 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                     }
                 } else if (h.type == T_FIXED) { /* FIXED order o as LPC, shift 0, 32-bit wrap (@0x10003810) */
                     const uint32_t o = h.order;
-                    c[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
-                    c[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
-                    c[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
-                    c[3] = o == 4 ? -1 : 0;
+                    cf[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
+                    cf[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
+                    cf[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
+                    cf[3] = o == 4 ? -1 : 0;
                 } else if (h.type == T_CONST) { /* order 1, coefficient 1, warm-up cval, zero residuals */
-                    c[0] = 1;
+                    cf[0] = 1;
                     order = 1;
                     row0[0] = h.cval;
                 }
-#pragma unroll
-                for (int t = 0; t < 32; t++) cf[t] = c[t];
                 pwasted = h.wasted;
                 const bool rice = h.type == T_FIXED || h.type == T_LPC;
                 rs.verb = rice ? 0u : 1u;
@@ -875,10 +809,26 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         const uint32_t nchunks = (mybs + SYS_CHK - 1u) / SYS_CHK;
         if (lane == 0) S.nchunks = nchunks;
         wait_vm(); /* setup loads and seeks done: the refill counts start from zero */
+        /* Ring refills (SYS_HELPERS): the restore waves fill the producer's ring.  At the end of
+         * chunk k the producer posts, per lane, the blocks from its issued end up to SYS_RD past
+         * its cursor's block, at most SYS_HB x SYS_CW of them (r_lo / r_hi, by chunk parity);
+         * restore iteration k + 1 loads them (global_load_dwordx4 per lane: one instruction per
+         * block index, where an LDS-DMA ring slot would take one per slot with ~1/8 of the lanes
+         * active) and iteration k + 2 writes them into the ring, so they are readable from chunk
+         * k + 3 on: rh1 / rh2 / rh3 = the lane's issued end after its request one / two / three
+         * chunks back.  The producer issues no memory op on the common path.  A lane that needs
+         * more than has landed (br_land) is starved: its frame goes to k_decode_list.  The ring
+         * keeps up with SYS_HB x SYS_CW blocks per 32 samples (32 bits per sample; C5: ~15). */
+        const bool helpers = sys_helpers(ablate);
+        uint32_t rh1 = b.iend, rh2 = b.iend, rh3 = b.iend;
+        if (helpers) b.hstarve = true;
         SysQ q;
-        q.d0 = q.d1 = q.d2 = 0;
-        q.e0 = q.e1 = q.e2 = b.iend;
+#pragma unroll
+        for (int i = 0; i < SYS_RQMAX; i++) q.d[i] = 0;
+#pragma unroll
+        for (int i = 0; i <= SYS_RQMAX; i++) q.e[i] = b.iend;
         q.tw = q.dw = 0;
+        const bool rf_chunk = !(ablate & 0x1000000u); /* refill once per chunk, 2 deep (ablate: every half, 4 deep) */
         sys_bar(); /* B0: tables ready */
         /* ================================================= producer: chunks */
         const bool tm = b.stats;
@@ -891,12 +841,18 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             if (k < nchunks) {
                 const uint32_t n0 = k * SYS_CHK;
                 int32_t *row = S.rows[k & 1u] + lane;
+                if (helpers) b.vendw = max(b.vendw, rh3 * 4u); /* the request of chunk k - 3 has landed */
 #pragma unroll
                 for (uint32_t hh = 0; hh < SYS_CHK / SYS_HALF; hh++) {
                     const uint32_t h0 = n0 + SYS_HALF * hh;
                     STAT(b.stats && active && h0 < bs, 4);
                     const uint64_t t0 = sys_now(tm);
-                    if (!(ablate & 0x80000u)) sys_refill(b, active && h0 < bs, q, tm); /* ablation: landings only */
+                    if (helpers || (ablate & 0x80000u)) { /* helpers / ablation: landings only */
+                    } else if (rf_chunk) {
+                        if (hh == 0) sys_refill<1>(b, active && h0 < bs, q, tm);
+                    } else {
+                        sys_refill<3>(b, active && h0 < bs, q, tm);
+                    }
                     const uint64_t t1 = sys_now(tm);
                     /* a run of SYS_HALF codewords of one Rice partition on every lane still decoding
                      * (partitions of 16 or more samples start on a run: their sizes are powers of
@@ -912,18 +868,11 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                         for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor(kmax, o));
                         kdirty = false;
                     }
-                    if (fast && any_lane(run) && !(ablate & 0x800000u)) {
+                    if (fast && any_lane(run)) {
                         const uint32_t kk = run ? rs.k : 0u;
                         /* every word the run can reach has landed */
                         if (__builtin_expect(any_lane(run && b.wi + 2u + SYS_HALF >= b.vendw), 0)) {
-                            STAT(b.stats, 2);
-                            wait_vm();
-                            b.vendw = b.iend * 4u;
-                            if (b.wi + 2u + SYS_HALF >= b.vendw) {
-                                br_refill(b);
-                                wait_vm();
-                                br_drained(b);
-                            }
+                            br_land(b, 2u + SYS_HALF);
                             b.nx = ring_word(b, b.wi);
                         }
                         int32_t *rrow = row + (h0 - n0) * SYS_RP;
@@ -935,16 +884,6 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                                 for (uint32_t i = got; i < SYS_HALF; i++) rrow[i * SYS_RP] = rice_one<true>(b, kk, limit, trunc);
                         }
                         if (run) rs.left -= SYS_HALF;
-                    } else if (fast && any_lane(run)) {
-                        int32_t r[SYS_HALF];
-                        const uint32_t kk = run ? rs.k : 0u;
-                        if (kmax <= 9u) sys_rice_run<true>(b, run, kk, 31u - kk, kk + 1u, 32u - kk, r, limit, trunc, lane);
-                        else sys_rice_run<false>(b, run, kk, 31u - kk, kk + 1u, 32u - kk, r, limit, trunc, lane);
-                        if (run) {
-                            rs.left -= SYS_HALF;
-#pragma unroll
-                            for (int i = 0; i < SYS_HALF; i++) row[(h0 - n0 + (uint32_t)i) * SYS_RP] = r[i];
-                        }
                     } else {
                         kdirty = true; /* rice_fused may read partition headers */
                         const uint32_t lo = max(h0, order), hi = active ? min(h0 + SYS_HALF, bs) : 0u;
@@ -958,6 +897,17 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                     t_ref += t1 - t0;
                     t_dec += t2 - t1;
                 }
+                if (helpers) { /* post this chunk's ring request */
+                    const bool want = active && n0 + SYS_CHK < bs;
+                    const uint32_t cb = b.wi >> 2;
+                    const uint32_t lo = max(b.iend, cb), hi = min(cb + SYS_RD, lo + SYS_HB * SYS_CW);
+                    S.r_lo[k & 1u][lane] = want ? lo : 0u;
+                    S.r_hi[k & 1u][lane] = want ? hi : 0u;
+                    if (want) b.iend = max(b.iend, hi);
+                    rh3 = rh2;
+                    rh2 = rh1;
+                    rh1 = want ? max(rh1, hi) : rh1;
+                }
             }
             const uint64_t t3 = sys_now(tm);
             sys_bar();
@@ -969,6 +919,10 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             atomicAdd(&g_stats[10], (unsigned long long)t_bar);
             atomicAdd(&g_sys_dbg[0], (unsigned long long)q.tw);
             atomicAdd(&g_sys_dbg[1], (unsigned long long)q.dw);
+        }
+        if (helpers) { /* the helpers' ring writes ended at the last loop barrier: refills are ours again */
+            if (b.starved) S.f_bad[fl] = 1u;
+            b.hstarve = false;
         }
         /* ================================================= producer: tail (read_frame_ @0x100118c0) */
         const bool last = active && ch + 1u == fi.channels;
@@ -1008,6 +962,7 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
 
     /* ===================================================== restore waves */
     const uint32_t w = wave - 1u;
+    const uint32_t nblk = (uint32_t)((nbytes + 15u) >> 4);
     sys_bar(); /* B0 */
     const uint32_t nchunks = S.nchunks;
     {
@@ -1018,10 +973,10 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         for (int o = 32; o > 0; o >>= 1) ord = max(ord, (uint32_t)__shfl_xor(ord, o));
         const bool any_w = any_lane(act && (fl & SF_WIDE)), any_n = any_lane(act && !(fl & SF_WIDE));
         const int pm = (ablate & 0x40000u) ? PM_MIXED : any_w ? (any_n ? PM_MIXED : PM_WIDE) : PM_NARROW;
-        if (ord <= 4u) sys_restore_pm<1>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate);
-        else if (ord <= 8u) sys_restore_pm<2>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate);
-        else if (ord <= 16u) sys_restore_pm<4>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate);
-        else sys_restore_pm<8>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate);
+        if (ord <= 4u) sys_restore_pm<1>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate, words, nblk);
+        else if (ord <= 8u) sys_restore_pm<2>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate, words, nblk);
+        else if (ord <= 16u) sys_restore_pm<4>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate, words, nblk);
+        else sys_restore_pm<8>(S, w, lane, lg, nchunks, fmt, sp, out, pm, ablate, words, nblk);
     }
     sys_bar(); /* tail done: frame table complete, CRC tables in rows[0] */
     /* ---- CRC-16 check, records, zero fill, hand-back (this wave's frames) */

@@ -106,7 +106,8 @@ typedef struct {
     uint64_t out_sample;
     uint32_t crc8, crc16_calc, crc16_read, crc_ok;
     uint32_t sub_start[8];
-    uint32_t flags;
+    uint32_t flags;         /* bit 1: past out_bytes (status 3), bit 2: layout cannot carry it (status 3); the other
+                               bits record the decode path (which kernel, hand-backs) and differ between paths */
     uint32_t crc_next;      /* k_parse's CRC pass: bit31 valid, bit30 CRC-16 of [frame_off, next offset) is 0,
                                bits 0-29 that length (0 when not computed) */
 } bnflac_frame_info;
