@@ -135,10 +135,6 @@ struct BR {
     uint32_t iend_old;              /* k_decode's 2-deep DMA pipeline: issued two refills ago */
     uint32_t ra, vlim;              /* k_decode_st: ring byte address of word wi (with the lane's bits), vendw - 1 */
     bool stats;
-    /* k_decode_sys: hstarve -- other waves of the workgroup fill this wave's ring, so it must
-     * not refill it itself; a lane that needs more than has landed is marked starved (its frame
-     * is handed back) and reads on without a guarantee. */
-    bool hstarve, starved;
 };
 
 DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, uint32_t lane, uint32_t rdepth) {
@@ -149,7 +145,6 @@ DEV void br_init(BR &b, const uint32_t *words, uint64_t nbytes, lds_u32 *ring, u
     b.nw = b.nblk * 4u;
     b.ring = ring;
     b.lring = ring + lane * 4u;
-    b.hstarve = b.starved = false;
     b.wi = 2;
     b.s = b.hi = b.lo = b.nx = 0;
     b.vendw = b.iend = 0;
@@ -198,22 +193,11 @@ DEV void dma_check_base(const lds_u32 *base) {
     (void)base;
 #endif
 }
-/* One LDS-DMA (16 bytes per lane to dst + 16 lane), issued as inline asm.  With the builtin
- * (__builtin_amdgcn_global_load_lds) anywhere in a loop, hipcc's waitcnt pass counts the DMA as an
- * LDS event on lgkmcnt too and waits lgkmcnt(0) before every LDS read in that loop: a ring word
- * read a step ahead was waited for at once, so the lookahead hid nothing.  Hidden from the pass,
- * the DMA is ordered by the kernels' own vmcnt waits (every ring word is read only below vendw,
- * the landed limit), and the pass keeps exact lgkmcnt counts for the LDS reads.  M0 holds the
- * wave-uniform LDS base (saved and restored: the compiler reserves M0 and may keep a value in it),
- * with one wait state between the M0 write and the DMA (the M0 hazard). */
+/* One LDS-DMA: 16 bytes per lane to dst + 16 lane.  (Issued as inline asm instead, hidden from
+ * the waitcnt pass, it measured 1-2% slower on k_decode_st in round 4.) */
 DEV void lds_dma16(const void *g, lds_u32 *dst) {
     dma_check_base(dst);
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(m0)
-                 : "memory");
+    __builtin_amdgcn_global_load_lds((gvoid *)g, (lds_void *)dst, 16, 0, 0);
 }
 DEV void dma_block(const BR &b, uint32_t j, uint32_t slot) { /* one 16-byte block per lane */
     lds_dma16(b.w + (uint64_t)min(j, b.nblk - 1u) * 4u, b.ring + slot * RING_LANE_DW);
@@ -231,7 +215,7 @@ DEV void br_refill(BR &b) {
     const uint32_t need = b.rdepth >= 8u ? ((b.wi >> 2) & ~3u) : (b.wi >> 2);
     const uint32_t lo = max(b.iend, need), hi = need + b.rdepth;
 #pragma unroll 1 /* rare path (seeks, landings), inlined at every cursor advance: keep it small */
-    for (int s = 0; s < 32; s++) { /* k_decode_sys's ring has 32 slots */
+    for (int s = 0; s < RING_MAX; s++) {
         if ((uint32_t)s >= b.rdepth) break; /* wave-uniform */
         const uint32_t j = lo + (((uint32_t)s - lo) & (b.rdepth - 1u));
         if (j < hi) dma_block(b, j, (uint32_t)s);
@@ -247,13 +231,6 @@ DEV void br_drained(BR &b) { /* every vector-memory op of this wave has complete
 }
 DEV void br_land(BR &b, uint32_t margin = 0) { /* afterwards words wi .. wi + margin have landed */
     STAT(b.stats, 2);
-    if (b.hstarve) { /* k_decode_sys's producer inside its chunk loop */
-        if (b.wi + margin >= b.vendw) {
-            b.starved = true;
-            b.vendw = b.wi + margin + 1u;
-        }
-        return;
-    }
     wait_vm();
     br_drained(b);
     if (b.wi + margin >= b.vendw) {
@@ -356,10 +333,15 @@ struct PendW {
     bool on;
 };
 DEV bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; } /* wave-uniform */
-/* leading zeros, ~0u for 0: one v_ffbh_u32 (LLVM folds the select into it).  Not inline asm: an
- * asm statement in a loop makes hipcc's waitcnt pass wait lgkmcnt(0) around it, so every LDS read
- * in flight (the ring lookahead) was waited for at each codeword. */
-DEV uint32_t ffbh(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : ~0u; }
+/* leading zeros, ~0u for 0 (v_ffbh_u32; asm so the compiler assumes no range).  An asm
+ * statement makes hipcc's waitcnt pass wait lgkmcnt(0) before it; the builtin form
+ * (x ? clz(x) : ~0u, also one v_ffbh_u32) keeps counted waits but measured 1-2% slower on
+ * k_decode_st (round 4) and no different on k_decode_sys. */
+DEV uint32_t ffbh(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 
 
 template <bool CHECK = true>

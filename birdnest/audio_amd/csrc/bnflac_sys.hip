@@ -52,20 +52,11 @@
 #define SYS_RP 80                    /* row stride (dwords), [sample][slot]: 80 = 16 mod 64 banks */
 #define SYS_CW 4                     /* restore waves per workgroup (16 subframe slots each) */
 #define SYS_THREADS (64 * (1 + SYS_CW))
-/* ring refills by the restore waves (1) or by the producer (0): see the producer's chunk loop */
-#ifndef SYS_HELPERS
-#define SYS_HELPERS 0
-#endif
-#ifndef SYS_RD                       /* producer ring: 16-byte blocks per lane */
-#define SYS_RD (SYS_HELPERS ? 32 : 16)
-#endif
+#define SYS_RD 16                    /* producer ring: 16-byte blocks per lane (256 B ahead of the cursor) */
 #define SYS_HALF 16                  /* producer step: residuals per refill and per fast run */
 #define SYS_CS 33                    /* coefficient table stride per slot (bank spread) */
-#define SYS_HB 2                     /* ring blocks each restore wave loads per producer lane and chunk */
 
 static_assert(SYS_CHK == 32, "the restore chunk is written for 32 samples (8 per quad lane)");
-static_assert(SYS_HB == 2, "the helpers' in-flight test is written for two blocks");
-DEV bool sys_helpers(uint32_t ablate) { return SYS_HELPERS == 1 || (SYS_HELPERS == 2 && !(ablate & 0x2000000u)); }
 static_assert(64 * SYS_CS * 4 <= SYS_CHK * SYS_RP * 4, "the coefficient table overlays row buffer 1");
 static_assert((8 * 256 + 512) * 2 <= SYS_CHK * SYS_RP * 4, "the CRC tables overlay row buffer 0");
 
@@ -80,7 +71,6 @@ enum { FS_NONE = 0, FS_DEC = 1, FS_TAIL = 2 };
 struct SysShared {
     uint32_t ring[SYS_RD * RING_LANE_DW];  /* producer bit rings: LDS-DMA images, 1 KiB aligned (first) */
     int32_t rows[2][SYS_CHK * SYS_RP];     /* residuals in, samples out; [1] holds the coefficients at setup */
-    uint32_t r_lo[2][64], r_hi[2][64];     /* the producer's ring requests by chunk parity: blocks [lo, hi) per lane */
     uint32_t p_order[64], p_sh[64], p_flags[64], p_wasted[64], p_bs[64];
     uint32_t f_idx[64], f_bs[64], f_ch[64], f_as[64], f_state[64], f_end[64], f_crc[64], f_bad[64];
     uint64_t f_os[64], f_off[64], f_resume[64];
@@ -464,7 +454,7 @@ DEV void sys_pack_prep(SysPk &k, const SysShared &S, uint32_t w, uint32_t lane, 
     }
 }
 /* one chunk; false: the generic pack must run (a frame ends part-way through this chunk) */
-DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt, uint8_t *__restrict__ out, uint32_t &nst) {
+DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt, uint8_t *__restrict__ out) {
     if (!k.ok) return false;
     if (any_lane((k.pv[0] && n0 < k.bs[0] && n0 + SYS_CHK > k.bs[0]) || (k.pv[1] && n0 < k.bs[1] && n0 + SYS_CHK > k.bs[1])))
         return false;
@@ -473,7 +463,6 @@ DEV bool sys_pack_fast(const SysPk &k, const int32_t *row, uint32_t n0, int fmt,
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         if (!any_lane(k.pv[r] && n0 < k.bs[r])) continue; /* piece 0's frame may be out while piece 1's decodes */
-        nst++; /* one store instruction below (wave-uniform) */
         if (!k.pv[r] || n0 >= k.bs[r]) continue;
         uint32_t s0 = k.s0[r], p = k.p[r];
         const uint32_t as = k.as[r];
@@ -572,34 +561,12 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
     SysPk pk;
     sys_pack_prep(pk, S, w, lane, lg, fmt, sp);
     const bool tm = (ablate & 0x100u) != 0;
-    const bool helpers = sys_helpers(ablate); /* this wave loads SYS_HB of each producer lane's ring blocks per chunk */
-    uint32_t nst = 0;                         /* store instructions of the last iteration's pack (fast pack: counted) */
-    /* ring blocks in flight: loaded after an iteration's restore steps, written into the ring at
-     * the start of the next (the pack and the barrier wait of latency cover; only the pack's
-     * stores, all younger, may then still be in flight).  Not live across the restore steps,
-     * where the VGPR count peaks (occupancy: 4 waves per SIMD hold two workgroups per CU). */
-    u32x4 hv[SYS_HB];
     uint64_t t_st = 0, t_pk = 0, t_bw = 0;
     sys_bar(); /* end of iteration 0: the producer's chunk 0 is in rows[0]; rows[1] may be overwritten */
     for (uint32_t k = 1; k <= nchunks; k++) {
         const uint64_t t0 = sys_now(tm);
         const uint32_t n0 = (k - 1u) * SYS_CHK;
         int32_t *row = S.rows[(k - 1u) & 1u];
-        /* the producer's ring request of chunk k - 2 (blocks [lo, hi) of each of its lanes), loaded
-         * by the last iteration: into the ring (lane l's block b: slot b mod SYS_RD, the LDS-DMA
-         * image layout) */
-        if (helpers && k >= 2u) {
-            const uint32_t lo = S.r_lo[k & 1u][lane], hi = S.r_hi[k & 1u][lane];
-            if (any_lane(lo + w < hi)) {
-                wait_vm_n(nst);
-#pragma unroll
-                for (int i = 0; i < SYS_HB; i++) {
-                    const uint32_t bl = lo + w + SYS_CW * (uint32_t)i;
-                    if (bl < hi) *(lds_u32x4 *)((lds_u32 *)S.ring + ((bl & (SYS_RD - 1u)) * 64u + lane) * 4u) = hv[i];
-                }
-            }
-        }
-        nst = 0;
         int32_t v[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) v[q] = row[(j + 4u * q) * SYS_RP + pl];
@@ -614,24 +581,10 @@ DEV void sys_restore(SysShared &S, uint32_t w, uint32_t lane, uint32_t lg, uint3
                 if (mmx && v[q] != (int32_t)(int16_t)v[q]) range_bad = true;
             }
         }
-        /* the producer's ring request of chunk k - 1: this wave's blocks lo + w + SYS_CW i */
-        if (helpers) {
-            uint32_t lo = S.r_lo[(k - 1u) & 1u][lane];
-            const uint32_t hi = S.r_hi[(k - 1u) & 1u][lane];
-            asm volatile("" : "+v"(lo)); /* keeps the loads below the restore steps (hv live there: VGPR peak) */
-#pragma unroll
-            for (int i = 0; i < SYS_HB; i++) {
-                const uint32_t bl = lo + w + SYS_CW * (uint32_t)i;
-                if (bl < hi) hv[i] = *(const __attribute__((address_space(1))) u32x4 *)(words + (uint64_t)min(bl, nblk - 1u) * 4u);
-            }
-        }
         lds_sync();
         const uint64_t t1 = sys_now(tm);
         if (!(ablate & 2u)) {
-            if ((ablate & 0x400000u) || !sys_pack_fast(pk, row, n0, fmt, out, nst)) {
-                sys_pack(S, row, w, lane, lg, n0, fmt, sp, out);
-                nst = 0; /* uncounted stores: the next wait takes them all */
-            }
+            if ((ablate & 0x400000u) || !sys_pack_fast(pk, row, n0, fmt, out)) sys_pack(S, row, w, lane, lg, n0, fmt, sp, out);
         }
         const uint64_t t2 = sys_now(tm);
         sys_bar();
@@ -809,19 +762,6 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         const uint32_t nchunks = (mybs + SYS_CHK - 1u) / SYS_CHK;
         if (lane == 0) S.nchunks = nchunks;
         wait_vm(); /* setup loads and seeks done: the refill counts start from zero */
-        /* Ring refills (SYS_HELPERS): the restore waves fill the producer's ring.  At the end of
-         * chunk k the producer posts, per lane, the blocks from its issued end up to SYS_RD past
-         * its cursor's block, at most SYS_HB x SYS_CW of them (r_lo / r_hi, by chunk parity);
-         * restore iteration k + 1 loads them (global_load_dwordx4 per lane: one instruction per
-         * block index, where an LDS-DMA ring slot would take one per slot with ~1/8 of the lanes
-         * active) and iteration k + 2 writes them into the ring, so they are readable from chunk
-         * k + 3 on: rh1 / rh2 / rh3 = the lane's issued end after its request one / two / three
-         * chunks back.  The producer issues no memory op on the common path.  A lane that needs
-         * more than has landed (br_land) is starved: its frame goes to k_decode_list.  The ring
-         * keeps up with SYS_HB x SYS_CW blocks per 32 samples (32 bits per sample; C5: ~15). */
-        const bool helpers = sys_helpers(ablate);
-        uint32_t rh1 = b.iend, rh2 = b.iend, rh3 = b.iend;
-        if (helpers) b.hstarve = true;
         SysQ q;
 #pragma unroll
         for (int i = 0; i < SYS_RQMAX; i++) q.d[i] = 0;
@@ -841,13 +781,12 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             if (k < nchunks) {
                 const uint32_t n0 = k * SYS_CHK;
                 int32_t *row = S.rows[k & 1u] + lane;
-                if (helpers) b.vendw = max(b.vendw, rh3 * 4u); /* the request of chunk k - 3 has landed */
 #pragma unroll
                 for (uint32_t hh = 0; hh < SYS_CHK / SYS_HALF; hh++) {
                     const uint32_t h0 = n0 + SYS_HALF * hh;
                     STAT(b.stats && active && h0 < bs, 4);
                     const uint64_t t0 = sys_now(tm);
-                    if (helpers || (ablate & 0x80000u)) { /* helpers / ablation: landings only */
+                    if (ablate & 0x80000u) { /* ablation: landings only */
                     } else if (rf_chunk) {
                         if (hh == 0) sys_refill<1>(b, active && h0 < bs, q, tm);
                     } else {
@@ -897,17 +836,6 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
                     t_ref += t1 - t0;
                     t_dec += t2 - t1;
                 }
-                if (helpers) { /* post this chunk's ring request */
-                    const bool want = active && n0 + SYS_CHK < bs;
-                    const uint32_t cb = b.wi >> 2;
-                    const uint32_t lo = max(b.iend, cb), hi = min(cb + SYS_RD, lo + SYS_HB * SYS_CW);
-                    S.r_lo[k & 1u][lane] = want ? lo : 0u;
-                    S.r_hi[k & 1u][lane] = want ? hi : 0u;
-                    if (want) b.iend = max(b.iend, hi);
-                    rh3 = rh2;
-                    rh2 = rh1;
-                    rh1 = want ? max(rh1, hi) : rh1;
-                }
             }
             const uint64_t t3 = sys_now(tm);
             sys_bar();
@@ -919,10 +847,6 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             atomicAdd(&g_stats[10], (unsigned long long)t_bar);
             atomicAdd(&g_sys_dbg[0], (unsigned long long)q.tw);
             atomicAdd(&g_sys_dbg[1], (unsigned long long)q.dw);
-        }
-        if (helpers) { /* the helpers' ring writes ended at the last loop barrier: refills are ours again */
-            if (b.starved) S.f_bad[fl] = 1u;
-            b.hstarve = false;
         }
         /* ================================================= producer: tail (read_frame_ @0x100118c0) */
         const bool last = active && ch + 1u == fi.channels;
