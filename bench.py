@@ -690,7 +690,8 @@ def c5_summary(r, args, world, steps=None):
     step_ms = r["t_dec"] / steps * 1e3
     out = {"value": round(r["samples"] * steps / r["t_dec"] / 1e6, 2), "unit": "MSamples/s",
            "ms_per_step": round(step_ms, 4), "bitexact": r["ok"], "files": r["files"], "ranks": world,
-           "roofline": roofline(r["alg_bytes_rank"], r["t_decode"], r["t_parse"], step_ms),
+           "roofline": roofline(r["alg_bytes_rank"], r["t_decode"], r["t_parse"], step_ms,
+                                measured_traffic("C5", r["files"], CONFIGS["C5"]["frames"]) if world == 1 else None),
            "with_gather": {"value": round(r["samples"] * steps / r["t_all"] / 1e6, 2), "unit": "MSamples/s",
                            "ms_per_step": round(r["t_all"] / steps * 1e3, 4),
                            "note": "each step: decode, then shard.gather_bytes of every rank's PCM to rank 0"},

@@ -2,10 +2,12 @@
 # Round-end measurement session (one gpurun call): every GPU test, a rocprofv3 kernel trace
 # + stats of each config's bench run, and the PMC passes (counters only, one rocprofv3 run
 # per pass) that tools/pmc_summary.py turns into profiles/traffic_<cfg>_b<B>.json.
-#   TAG=r3final bash tools/final_r3.sh        (outputs under gpurun_out/)
+#   TAG=r4final bash tools/final_session.sh          (stage 1: tests + kernel traces)
+#   TAG=r4final STAGE=2 bash tools/final_session.sh  (stage 2: PMC passes + the default bench line)
+# C5 runs its real flow (bench.py --config C5: c5_job over 8 distinct files).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r3final}
+TAG=${TAG:-r4final}
 mkdir -p gpurun_out
 if [ "${STAGE:-1}" = 1 ]; then
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu \
@@ -13,15 +15,13 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/${TAG}_pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 for c in ${CFGS:-C2 C3 C4 C5}; do
-  x=""; [ $c = C5 ] && x="--c5-batch"   # the C5 leg's workload (8 files' frames in one batch)
-  TAG=$TAG CFG=$c STEPS=5 EXTRA="$x" bash tools/prof_cfg.sh > gpurun_out/${TAG}_prof_$c.txt 2>&1 || { cat gpurun_out/${TAG}_prof_$c.txt; exit 1; }
+  TAG=$TAG CFG=$c STEPS=5 bash tools/prof_cfg.sh > gpurun_out/${TAG}_prof_$c.txt 2>&1 || { cat gpurun_out/${TAG}_prof_$c.txt; exit 1; }
   head -8 gpurun_out/${TAG}_prof_$c.txt
 done
 echo "stage 1 done"; exit 0
 fi
 for c in ${CFGS:-C2 C3 C4 C5}; do
-  x=""; [ $c = C5 ] && x="--c5-batch"
-  PMC_BENCH_ARGS="--config $c $x --steps 2 --warmup 1 --legs= --no-cpu-baseline --no-pcie --no-index --no-reader" \
+  PMC_BENCH_ARGS="--config $c --steps 2 --warmup 1 --legs= --no-cpu-baseline --no-pcie --no-index --no-reader" \
   PMC_SETS='FETCH_SIZE
 WRITE_SIZE
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES' \
