@@ -114,6 +114,8 @@ DEV void gst128(uint64_t addr, u32x4 v) { *(__attribute__((address_space(1))) u3
 /* Mode bit: k_decode_list -- the frames of a device list (k_decode_sys's hand-backs), every
  * class, decoded by this instance (no class split, stereo fast-path frames included). */
 #define BNF_MODE_LIST 0x20000u
+/* Mode bit: k_decode_seg -- the W = 32 instance also takes the W16 class's blocks. */
+#define BNF_MODE_SEG 0x80000000u
 
 /* ----------------------------------------------------------------- bit reader */
 #define RING_MAX 16       /* 16-byte slots per lane (k_parse and k_decode_st use 8) */
@@ -1865,6 +1867,46 @@ __global__ void __launch_bounds__(256) k_crc_join(const uint8_t *__restrict__ by
         for (uint64_t i = 0; i < n; i++) out[start + i] = 0;
     }
 }
+
+/* The batch API's defined output for a frame whose status is not OK (bnflac_decode_parsed):
+ * after every decode kernel, the output range of each ERROR / TRUNC frame whose header
+ * parsed (sub_start[0] != 0: a CRC-8-checked header, so its position is the one the frame
+ * would have been written to) is zero-filled, as a CRC-failed frame is; a frame whose header
+ * did not parse has no range and is not written.  The lane kernels may have stored part of a
+ * frame before finding its error; this pass overwrites that.  One lane per frame reads the
+ * record; each bad frame is then filled by the whole wave (rare). */
+__global__ void __launch_bounds__(64) k_fill_bad(const bnf_frame_info *__restrict__ info, uint32_t nframes,
+                                                 bnf_stream_params sp, int fmt, uint8_t *__restrict__ out,
+                                                 uint64_t out_bytes) {
+    const uint32_t f = blockIdx.x * 64u + threadIdx.x;
+    bool bad = false;
+    uint64_t start = 0, n = 0;
+    if (f < nframes) {
+        const uint32_t st = info[f].status;
+        if ((st == BNF_ST_ERROR || st == BNF_ST_TRUNC) && info[f].sub_start[0] != 0u) {
+            const uint32_t C = info[f].channels, bsz = info[f].blocksize;
+            const uint64_t os = info[f].out_sample;
+            switch (fmt) {
+            case BNF_OUT_PLANAR32: start = os * sp.channels * 4u; n = (uint64_t)C * bsz * 4u; break;
+            case BNF_OUT_INTERLEAVED32: start = os * sp.channels * 4u; n = (uint64_t)sp.channels * bsz * 4u; break;
+            case BNF_OUT_FLACDECODER: start = os * (C == 2 ? 4u : 2u); n = (uint64_t)bsz * (C == 2 ? 4u : 2u); break;
+            default: {
+                const uint32_t fb = sp.bps == 24 ? 3u : 2u;
+                start = os * sp.channels * fb;
+                n = (uint64_t)bsz * sp.channels * fb;
+            }
+            }
+            bad = n != 0 && start <= out_bytes && n <= out_bytes - start;
+        }
+    }
+    uint64_t m = __ballot(bad);
+    while (m) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1u;
+        const uint64_t s0 = __shfl(start, l), n0 = __shfl(n, l);
+        for (uint64_t i = threadIdx.x; i < n0; i += 64u) out[s0 + i] = 0;
+    }
+}
 #endif
 
 /* Channel decorrelation (read_frame_ @0x10011a37-0x10011adb), 32-bit wrap. */
@@ -2189,7 +2231,7 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
         const bool a32 = __any(frame_ok && !st_frame && (fi.flags & BNF_FL_W32)) != 0;
         const bool a16 = __any(frame_ok && !st_frame && (fi.flags & BNF_FL_W16)) != 0;
         const int cls = a32 ? 32 : (a16 ? 16 : 8);
-        if (cls != MAXW) {
+        if (cls != MAXW && !(MAXW == 32 && cls == 16 && (ablate & BNF_MODE_SEG))) {
             if (MAXW != 8) return;
             have = have && st_frame; /* a W16/W32 block: only its handed-back ST frames */
             frame_ok = frame_ok && st_frame;
@@ -2607,6 +2649,30 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode_list(const uint32_t *__
     for (uint32_t blk = blockIdx.x; blk < nb; blk += gridDim.x) {
         decode_block<MAXW, CHK, RD>(blk, ring, lds, words, nbytes, cnt, sp, chn_lanes, fmt, out, out_bytes, info, list + 4,
                                     ablate | BNF_MODE_LIST | BNF_MODE_WREDO);
+        __syncthreads();
+    }
+}
+
+/* The W16 and W32 classes of the decode order in one small grid striding over their blocks
+ * (seg: k_order's bucket ends, classes 2 and 3 are adjacent), the usual class rules.  Launched
+ * instead of the two full-size side grids when the previous batch had no such frames (C2):
+ * an empty segment costs two loads per workgroup of a 512-workgroup launch, where the side
+ * grids were 32,768 early-exiting waves each. */
+template <int MAXW, int CHK, int RD>
+__global__ void __launch_bounds__(DEC_LANES, 2) k_decode_seg(const uint32_t *__restrict__ words, uint64_t nbytes,
+                                                          uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
+                                                          int fmt, uint8_t *__restrict__ out, uint64_t out_bytes,
+                                                          bnf_frame_info *__restrict__ info,
+                                                          const uint32_t *__restrict__ perm, uint32_t ablate,
+                                                          const uint32_t *__restrict__ seg) {
+    __shared__ LDS_DMA_ALIGN uint32_t ring[RD * RING_LANE_DW];
+    __shared__ int32_t lds[CHK * RP];
+    const uint32_t fpb = DEC_LANES >> __builtin_ctz(chn_lanes);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(seg[2u * 64u - 1u]) / fpb;
+    const uint32_t end = (__builtin_amdgcn_readfirstlane(seg[3u * 64u + 63u]) + fpb - 1u) / fpb;
+    for (uint32_t blk = lo + blockIdx.x; blk < end; blk += gridDim.x) {
+        decode_block<MAXW, CHK, RD>(blk, ring, lds, words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info,
+                                    perm, ablate);
         __syncthreads();
     }
 }
@@ -3838,6 +3904,64 @@ DEV void sw_decor(uint32_t as, int32_t &l, int32_t &r) {
     else decorrelate((uint32_t)AS, l, r);
 }
 
+/* FLACFileReader's 24-bit LE pack of 8 stereo samples (FLACFileReader.cs:230-237): 48 bytes */
+DEV void sw_pack24(const int32_t (&L)[8], const int32_t (&R)[8], uint32_t (&d)[12]) {
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        const uint32_t l0 = (uint32_t)L[2 * h], r0 = (uint32_t)R[2 * h], l1 = (uint32_t)L[2 * h + 1], r1 = (uint32_t)R[2 * h + 1];
+        d[3 * h] = __builtin_amdgcn_perm(r0, l0, 0x04020100u);     /* l0.b0 l0.b1 l0.b2 r0.b0 */
+        d[3 * h + 1] = __builtin_amdgcn_perm(l1, r0, 0x05040201u); /* r0.b1 r0.b2 l1.b0 l1.b1 */
+        d[3 * h + 2] = __builtin_amdgcn_perm(r1, l1, 0x06050402u); /* l1.b2 r1.b0 r1.b1 r1.b2 */
+    }
+}
+
+/* The FLACFileReader line flush (C3).  A 16-sample chunk is 96 bytes of a frame's run, so two
+ * chunks are three 64-byte lines: an even chunk completes line 0 and leaves the first half of
+ * line 1 (carry), an odd chunk completes lines 1 and 2.  Each lane puts a line's four 16-byte
+ * units into its own 64-byte LDS slot; the flush then has every lane store one unit of the
+ * line of frame (lane >> 2) + 16 i, i = 0..3: four stores of sixteen whole lines each, instead
+ * of per-lane 16-byte stores scattered over 64 lines.  Cross-lane reads (the slots, the run
+ * addresses by ds_bpermute) happen only at chunk end with every lane active: inside a chunk a
+ * lane whose frame has ended is masked off, and a read of its registers would yield nothing. */
+struct SwLn {
+    u32x4 c0, c1;     /* even chunk: the carried first half of line 1 */
+    u32x4 h0, h1, h2, h3; /* odd chunk: line 2 (a2 from the first group, b0..b2 from the second) */
+};
+DEV void sw_line_group(lds_u32x4 *stg, uint32_t lane, bool odd, bool carry, SwLn &q, const uint32_t (&d)[12],
+                       int g, uint8_t *run) {
+    const u32x4 u0 = u32x4{d[0], d[1], d[2], d[3]}, u1 = u32x4{d[4], d[5], d[6], d[7]}, u2 = u32x4{d[8], d[9], d[10], d[11]};
+    lds_u32x4 *my = stg + lane * 4u;
+    if (!odd) {
+        if (g == 0) { my[0] = u0; my[1] = u1; my[2] = u2; }
+        else { my[3] = u0; q.c0 = u1; q.c1 = u2; }
+    } else if (g == 0) {
+        if (carry) { my[0] = q.c0; my[1] = q.c1; my[2] = u0; my[3] = u1; }
+        else { /* no carried half: the first half of line 1 was stored directly */
+            gst128((uint64_t)(uintptr_t)run, u0);
+            gst128((uint64_t)(uintptr_t)run + 16u, u1);
+        }
+        q.h0 = u2;
+    } else {
+        q.h1 = u0; q.h2 = u1; q.h3 = u2;
+    }
+}
+/* every lane active: the slots' line of each frame to base(frame) (0: not stored); returns
+ * the store instructions issued */
+DEV uint32_t sw_line_flush(const lds_u32x4 *stg, uint64_t base, uint32_t lane) {
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        const uint32_t src = (lane >> 2) + 16u * i;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)base);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)(base >> 32));
+        const uint64_t a = ((uint64_t)hi << 32) | lo;
+        const u32x4 v = stg[src * 4u + (lane & 3u)];
+        if (a) gst128(a + 16u * (lane & 3u), v);
+        if (any_lane(a != 0)) n++;
+    }
+    return n;
+}
+
 /* 8 stereo samples n..n+7 of this lane's frame (nv valid) into the layout; al: 16-byte
  * aligned runs (then 3 or 4 16-byte stores).  Returns whether the aligned path stored. */
 template <int FMT>
@@ -3845,13 +3969,7 @@ DEV bool sw_emit8(uint8_t *dst, uint32_t n, uint32_t nv, bool al, uint32_t bs, c
     if (nv == 0) return false;
     if (FMT == BNF_OUT_FILEREADER) { /* 24-bit LE, L R L R ... */
         uint32_t d[12];
-#pragma unroll
-        for (int h = 0; h < 4; h++) {
-            const uint32_t l0 = (uint32_t)L[2 * h], r0 = (uint32_t)R[2 * h], l1 = (uint32_t)L[2 * h + 1], r1 = (uint32_t)R[2 * h + 1];
-            d[3 * h] = __builtin_amdgcn_perm(r0, l0, 0x04020100u);     /* l0.b0 l0.b1 l0.b2 r0.b0 */
-            d[3 * h + 1] = __builtin_amdgcn_perm(l1, r0, 0x05040201u); /* r0.b1 r0.b2 l1.b0 l1.b1 */
-            d[3 * h + 2] = __builtin_amdgcn_perm(r1, l1, 0x06050402u); /* l1.b2 r1.b0 r1.b1 r1.b2 */
-        }
+        sw_pack24(L, R, d);
         uint8_t *o = dst + (uint64_t)n * 6u;
         if (al && nv == 8) {
 #pragma unroll
@@ -3899,10 +4017,10 @@ template <int FMT> constexpr uint32_t sw_stores8() { return FMT == BNF_OUT_FILER
  * (k_decode_st's single step), the prediction from the older-tap sum of the previous step
  * plus the newest tap, the next sample's older taps, the history, and at T = 7 / 15 the 8
  * samples' wasted bits, decorrelation and stores. */
-template <int T, int FMT, int PATH, int AS>
+template <int T, int FMT, int PATH, int AS, int LN>
 DEV void sw_fused_step(StW &z0, StW &z1, int32_t (&L)[8], int32_t (&R)[8], uint64_t limit, uint32_t &trunc, uint32_t nq,
                        uint32_t as, uint8_t *dst, uint32_t nbase, bool al, uint32_t bs, bool sto, int64_t &pre0,
-                       int64_t &pre1, uint32_t lane) {
+                       int64_t &pre1, uint32_t lane, lds_u32x4 *stg, bool odd, bool carry, SwLn &q) {
     /* source order is issue order here (the compiler keeps its MAC asm blocks in place): the
      * two cursor chains first, the MAC blocks between their dependent steps */
     const uint32_t w0 = br_peek(z0.b), w1 = br_peek(z1.b);
@@ -3933,8 +4051,14 @@ DEV void sw_fused_step(StW &z0, StW &z1, int32_t (&L)[8], int32_t (&R)[8], uint6
     R[T & 7] = (int32_t)((uint32_t)s1 << z1.wasted);
     if ((T & 7) == 7) {
 #pragma unroll
-        for (int q = 0; q < 8; q++) sw_decor<AS>(as, L[q], R[q]);
-        if (sto) sw_emit8<FMT>(dst, nbase + (uint32_t)T - 7u, 8u, al, bs, L, R);
+        for (int i = 0; i < 8; i++) sw_decor<AS>(as, L[i], R[i]);
+        if (LN) { /* FILEREADER line flush: units to the LDS slot / carry (sw_line_group) */
+            uint32_t d[12];
+            sw_pack24(L, R, d);
+            sw_line_group(stg, lane, odd, carry, q, d, T >> 3, dst + (uint64_t)nbase * 6u);
+        } else if (sto) {
+            sw_emit8<FMT>(dst, nbase + (uint32_t)T - 7u, 8u, al, bs, L, R);
+        }
     }
 }
 
@@ -3993,6 +4117,10 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     const uint64_t os = ok ? fi.out_sample : 0u;
     ok = ok && (os + bs) * stride <= out_bytes;
     uint8_t *dst = out + os * stride;
+    /* timing ablation 0x10000000: every wave stores into one 64 KB window (same store
+     * instructions, an L2-resident footprint); output is wrong */
+    const bool hot = (ablate & 0x10000000u) != 0;
+    if (hot) dst = out + (uint64_t)(blockIdx.x & 7u) * 65536u + lane * 1024u;
     const bool al = (((uintptr_t)dst) & 15u) == 0 && (FMT != BNF_OUT_PLANAR32 || (bs & 3u) == 0);
     const bool all_al = !any_lane(ok && !al); /* every run of the wave takes the 16-byte stores */
 
@@ -4023,6 +4151,20 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
     const uint32_t nchunks = (mybs + ST_CHK - 1) / ST_CHK;
     uint32_t trunc = 0;
+    const bool sto = !(ablate & 2u);
+    /* FILEREADER runs that start on a 64-byte line: the fused chunks flush whole lines
+     * (sw_line_flush); the slots sit past the two rings (the CRC tables' extra 4 KB).
+     * Ablation bit 0x20000000 (exact): per-lane 16-byte stores instead */
+#ifndef BNF_SW_LINE
+#define BNF_SW_LINE 1
+#endif
+    const bool line = BNF_SW_LINE && FMT == BNF_OUT_FILEREADER && sto && !hot && all_al && !(ablate & 0x20000000u) &&
+                      !any_lane(ok && (((uintptr_t)dst) & 63u) != 0);
+    lds_u32x4 *stg = (lds_u32x4 *)((lds_u32 *)ring + 2u * ST_RD * RING_LANE_DW);
+    static_assert(sizeof(ring) >= (2u * ST_RD * RING_LANE_DW + 1024u) * 4u, "line slots past the rings");
+    SwLn q;
+    bool carry = false, cvalid = false; /* carry: an even chunk left its half line (wave-uniform) */
+    uint32_t carry_b = 0;                /* its byte offset in the runs */
     wait_vm(); /* setup loads done: the store count starts from zero */
     uint32_t nst = 0; /* vector-memory ops (PCM stores) issued by this wave since the last refill's DMAs (a lower bound) */
     for (uint32_t kc = 0; kc < nchunks; kc++) {
@@ -4035,33 +4177,74 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
             fast = !z0.esc && !z1.esc && z0.left >= ST_CHK && z1.left >= ST_CHK;
         }
         const bool fused = !any_lane(valid && !fast);
-        const bool sto = !(ablate & 2u);
+        const bool odd = (kc & 1u) != 0;
+        const bool ln = line && fused && any_lane(valid);
+        if (carry) { /* a carried half line that this chunk does not take: stored directly */
+            const bool take = ln && odd;
+            const bool d = cvalid && !(take && valid);
+            if (d) {
+                gst128((uint64_t)(uintptr_t)dst + carry_b, q.c0);
+                gst128((uint64_t)(uintptr_t)dst + carry_b + 16u, q.c1);
+            }
+            if (any_lane(d)) nst += 2u;
+            if (!take) carry = false;
+        }
         if (fused) {
             if (valid) {
                 int64_t pre0 = sw_pre<15>(z0), pre1 = sw_pre<15>(z1); /* older taps of the chunk's first sample */
                 st_resync(z0.b, lane);
                 st_resync(z1.b, lane);
-                auto chunk = [&](auto pc, auto ac) {
-                    constexpr int PATH = decltype(pc)::value, AS = decltype(ac)::value;
+                auto chunk = [&](auto pc, auto ac, auto lc) {
+                    constexpr int PATH = decltype(pc)::value, AS = decltype(ac)::value, LN = decltype(lc)::value;
 #pragma unroll 1
                     for (uint32_t h = 0; h < ST_CHK / 16; h++) {
                         int32_t L[8], R[8];
-                        const uint32_t nb = n0 + h * 16u;
-                        const uint32_t nqa = nst + (all_al && sto ? h * 2u * SPG : 0u);
-                        const uint32_t nqb = nqa + (all_al && sto ? SPG : 0u);
-#define SWS(T, NQ) sw_fused_step<T, FMT, PATH, AS>(z0, z1, L, R, limit, trunc, NQ, as, dst, nb, al, bs, sto, pre0, pre1, lane)
+                        const uint32_t nb = hot ? (n0 + h * 16u) & 127u : n0 + h * 16u;
+                        const uint32_t nqa = nst + (!LN && all_al && sto ? h * 2u * SPG : 0u);
+                        const uint32_t nqb = nqa + (LN ? 0u : (all_al && sto ? SPG : 0u));
+#define SWS(T, NQ) sw_fused_step<T, FMT, PATH, AS, LN>(z0, z1, L, R, limit, trunc, NQ, as, dst, nb, al, bs, sto, pre0, pre1, lane, stg, odd, carry, q)
                         SWS(0, nqa); SWS(1, nqa); SWS(2, nqa); SWS(3, nqa); SWS(4, nqa); SWS(5, nqa); SWS(6, nqa); SWS(7, nqa);
                         SWS(8, nqb); SWS(9, nqb); SWS(10, nqb); SWS(11, nqb); SWS(12, nqb); SWS(13, nqb); SWS(14, nqb); SWS(15, nqb);
 #undef SWS
                     }
                 };
-                if (fix == 3) chunk(std::integral_constant<int, 0>(), std::integral_constant<int, 3>());
-                else if (fix == 0) chunk(std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
-                else chunk(std::integral_constant<int, 2>(), std::integral_constant<int, -1>());
+                using I0 = std::integral_constant<int, 0>;
+                using I1 = std::integral_constant<int, 1>;
+                bool done = false;
+                if constexpr (FMT == BNF_OUT_FILEREADER) {
+                    if (ln) {
+                        if (fix == 3) chunk(I0(), std::integral_constant<int, 3>(), I1());
+                        else if (fix == 0) chunk(I0(), I0(), I1());
+                        else chunk(std::integral_constant<int, 2>(), std::integral_constant<int, -1>(), I1());
+                        done = true;
+                    }
+                }
+                if (!done) {
+                    if (fix == 3) chunk(I0(), std::integral_constant<int, 3>(), I0());
+                    else if (fix == 0) chunk(I0(), I0(), I0());
+                    else chunk(std::integral_constant<int, 2>(), std::integral_constant<int, -1>(), I0());
+                }
                 z0.left -= ST_CHK;
                 z1.left -= ST_CHK;
             }
-            if (all_al && sto && any_lane(valid)) nst += (ST_CHK / 8) * SPG;
+            if (ln) { /* every lane active: the chunk's lines (sw_line_flush) */
+                const uint64_t run = valid ? (uint64_t)(uintptr_t)dst + (uint64_t)n0 * 6u : 0ull;
+                if (!odd) {
+                    nst += sw_line_flush(stg, run, lane);
+                    carry = true;
+                    cvalid = valid;
+                    carry_b = n0 * 6u + 64u; /* units c0, c1: bytes 64..95 of the chunk */
+                } else {
+                    if (!carry) nst += 2u; /* the direct half line (sw_line_group) */
+                    if (carry) nst += sw_line_flush(stg, run ? run - 32u : 0ull, lane);
+                    lds_u32x4 *my = stg + lane * 4u;
+                    my[0] = q.h0; my[1] = q.h1; my[2] = q.h2; my[3] = q.h3;
+                    nst += sw_line_flush(stg, run ? run + 32u : 0ull, lane);
+                    carry = false;
+                }
+            } else if (all_al && sto && any_lane(valid)) {
+                nst += (ST_CHK / 8) * SPG;
+            }
         } else {
 #pragma unroll 1
             for (uint32_t h = 0; h < ST_CHK / 16; h++) {
@@ -4089,6 +4272,11 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
             st_refill_issue(z1.b, want);
             nst = 0;
         }
+    }
+
+    if (carry && cvalid) { /* the last chunk was even: its half line */
+        gst128((uint64_t)(uintptr_t)dst + carry_b, q.c0);
+        gst128((uint64_t)(uintptr_t)dst + carry_b + 16u, q.c1);
     }
 
     /* ---- end of the last subframe, zero padding, CRC-16 (read_frame_ tail) */
@@ -4219,6 +4407,16 @@ hipError_t bnf_launch_decode_list_tu2(const uint32_t *words, uint64_t nbytes, ui
                        chn_lanes, fmt, out, out_bytes, info, list, ablate_flags() | mode);
     return hipGetLastError();
 }
+/* the W16 + W32 segment of the decode order (k_decode_seg; perm and seg required) */
+hipError_t bnf_launch_decode_seg_tu2(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
+                                     uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
+                                     const uint32_t *perm, uint32_t mode, const uint32_t *seg, hipStream_t s) {
+    const uint32_t fpb = DEC_LANES / chn_lanes;
+    const uint32_t nb = std::min<uint32_t>((nframes + fpb - 1) / fpb, 512u);
+    hipLaunchKernelGGL((k_decode_seg<DEC_W, 32, DEC_RD>), dim3(std::max(nb, 1u)), dim3(DEC_LANES), 0, s, words, nbytes,
+                       nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, ablate_flags() | mode | BNF_MODE_SEG, seg);
+    return hipGetLastError();
+}
 #endif
 } /* extern "C" */
 #endif
@@ -4340,6 +4538,8 @@ hipError_t bnf_launch_decode_sys_tu8(const uint32_t *, uint64_t, uint32_t, bnf_s
                                      uint64_t, bnf_frame_info *, const uint32_t *, uint32_t *, uint32_t, hipStream_t);
 hipError_t bnf_launch_decode_list_tu2(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
                                       uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
+hipError_t bnf_launch_decode_seg_tu2(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
+                                     uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, const uint32_t *, hipStream_t);
 void bnf_set_ablate_tu1(uint32_t);
 void bnf_set_ablate_tu2(uint32_t);
 hipError_t bnf_stats_tu1(uint64_t *, int);
@@ -4448,7 +4648,9 @@ __global__ void __launch_bounds__(256) k_order_count(const bnf_frame_info *__res
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
-__global__ void __launch_bounds__(ORDER_NB) k_order_scan(uint32_t *__restrict__ hist) { /* exclusive, in place */
+/* exclusive, in place; cls (host memory, optional): the W16 and W32 class sizes, which
+ * bnf_launch_decode reads back one batch later to choose the side grids */
+__global__ void __launch_bounds__(ORDER_NB) k_order_scan(uint32_t *__restrict__ hist, uint32_t *__restrict__ cls) {
     __shared__ uint32_t t[ORDER_NB];
     const uint32_t i = threadIdx.x;
     const uint32_t v = hist[i];
@@ -4461,6 +4663,10 @@ __global__ void __launch_bounds__(ORDER_NB) k_order_scan(uint32_t *__restrict__ 
         __syncthreads();
     }
     hist[i] = t[i] - v;
+    if (cls && i == ORDER_NB - 1u) {
+        cls[0] = t[3u * 64u - 1u] - t[2u * 64u - 1u];
+        cls[1] = t[4u * 64u - 1u] - t[3u * 64u - 1u];
+    }
 }
 template <int MODE>
 __global__ void __launch_bounds__(256) k_order_place(const bnf_frame_info *__restrict__ info,
@@ -4484,13 +4690,14 @@ __global__ void __launch_bounds__(256) k_order_place(const bnf_frame_info *__res
 /* order: ORDER_NB + nframes words of scratch; returns the permutation inside it */
 template <int MODE>
 static hipError_t launch_order(const bnf_frame_info *info, const uint8_t *bytes, uint64_t nbytes, const uint64_t *offs,
-                               uint32_t nframes, uint32_t *order, const uint32_t **perm, hipStream_t s) {
+                               uint32_t nframes, uint32_t *order, const uint32_t **perm, hipStream_t s,
+                               uint32_t *cls = nullptr) {
     uint32_t *hist = order, *pm = order + ORDER_NB;
     hipError_t e = hipMemsetAsync(hist, 0, ORDER_NB * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     const dim3 g((nframes + 255) / 256);
     hipLaunchKernelGGL(k_order_count<MODE>, g, dim3(256), 0, s, info, bytes, nbytes, offs, nframes, hist);
-    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(ORDER_NB), 0, s, hist);
+    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(ORDER_NB), 0, s, hist, cls);
     hipLaunchKernelGGL(k_order_place<MODE>, g, dim3(256), 0, s, info, bytes, nbytes, offs, nframes, hist, pm);
     *perm = pm;
     return hipGetLastError();
@@ -4502,8 +4709,10 @@ static hipError_t launch_order(const bnf_frame_info *info, const uint8_t *bytes,
 struct SideQ {
     hipStream_t st[2]; /* W16, W32 */
     hipEvent_t fork, join[2];
+    uint32_t *cls; /* host memory: the last decode order's W16 / W32 class sizes (k_order_scan) */
 };
 static std::mutex g_side_mu;
+static std::atomic<uint64_t> g_seg_launches{0}; /* k_decode_seg launches (bnf_decode_seg_launches) */
 static SideQ g_side[64];
 static int decode_fork_mode() { /* 0 serial; 1 fork after k_decode_st; 2 fork before it (default) */
     static const int m = [] {
@@ -4524,6 +4733,8 @@ static SideQ *side_queue() { /* under g_side_mu; nullptr: decode serially */
         for (int i = 0; i < 2 && ok; i++)
             ok = hipStreamCreateWithFlags(&n.st[i], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&n.join[i], hipEventDisableTiming) == hipSuccess;
+        if (ok && hipHostMalloc((void **)&n.cls, 64, hipHostMallocCoherent) != hipSuccess) n.cls = nullptr;
+        if (n.cls) n.cls[0] = n.cls[1] = ~0u; /* unknown: the full grids */
         if (!ok) {
             for (int i = 0; i < 2; i++) {
                 if (n.join[i]) (void)hipEventDestroy(n.join[i]);
@@ -4584,6 +4795,7 @@ static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32
 }
 
 extern "C" {
+uint64_t bnf_decode_seg_launches() { return g_seg_launches.load(std::memory_order_relaxed); }
 void bnf_set_decode_sys(int mode) { g_decode_sys.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
 void bnf_set_parse_wave(int mode) { g_parse_wave.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
 hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset) { /* debug counters of k_parse_wave (BNFLAC_PW_STATS=1) */
@@ -4628,6 +4840,15 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
     return hipGetLastError();
 }
 
+/* k_fill_bad over a decoded batch (the batch API; not the stream API's candidate windows,
+ * whose failed candidates share the next frame's slot) */
+hipError_t bnf_launch_fill_bad(const bnf_frame_info *info, uint32_t nframes, bnf_stream_params sp, int fmt,
+                               uint8_t *out, uint64_t out_bytes, hipStream_t s) {
+    if (!nframes) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_bad, dim3((nframes + 63) / 64), dim3(64), 0, s, info, nframes, sp, fmt, out, out_bytes);
+    return hipGetLastError();
+}
+
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                              uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
                              uint32_t *order, hipEvent_t ev_crc, hipStream_t s) {
@@ -4646,14 +4867,8 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
             e = bnf_launch_decode_list_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, list, mode, s);
         return e;
     }
-    const uint32_t *perm = nullptr;
-    if (order) {
-        hipError_t e = launch_order<0>(info, nullptr, 0, nullptr, nframes, order, &perm, s);
-        if (e != hipSuccess) return e;
-    }
     /* the class segments of the decode order (bucket ends), for the W16 / W32 grids */
     static const bool seg_on = [] { const char *e = getenv("BNFLAC_DECODE_SEG"); return !e || atoi(e) != 0; }();
-    const uint32_t *seg = (perm && seg_on) ? order : nullptr;
     /* k_decode_st -> k_decode<8> on s (k_decode<8> takes k_decode_st's hand-backs);
      * k_decode<16> and k_decode<32> each on a side stream of the device, forked from s
      * before k_decode_st (default) or after it (BNFLAC_DECODE_FORK=1), and joined before
@@ -4677,7 +4892,20 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         lk.lock();
         sq = side_queue();
     }
+    /* W16 / W32 grids: the full-size side grids, or -- when the previous decode order on this
+     * device had neither class (read from host memory one batch behind, no sync; a stale or
+     * wrong guess only costs time) -- k_decode_seg over both classes after k_decode<8> */
+    uint32_t *cls = (sq && seg_on && order) ? sq->cls : nullptr;
+    const bool seg_only = cls && __atomic_load_n(&cls[0], __ATOMIC_RELAXED) == 0u &&
+                          __atomic_load_n(&cls[1], __ATOMIC_RELAXED) == 0u;
+    const uint32_t *perm = nullptr;
     hipError_t e = hipSuccess;
+    if (order) e = launch_order<0>(info, nullptr, 0, nullptr, nframes, order, &perm, s, cls);
+    const uint32_t *seg = (perm && seg_on) ? order : nullptr;
+    if (seg_only) { /* no fork */
+        sq = nullptr;
+        lk.unlock();
+    }
     auto fork = [&]() -> hipError_t {
         hipError_t r = hipEventRecord(sq->fork, s);
         for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipStreamWaitEvent(sq->st[i], sq->fork, 0);
@@ -4688,7 +4916,7 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipEventRecord(sq->join[i], sq->st[i]);
         return r;
     };
-    if (sq && fm == 2) e = fork();
+    if (sq && fm == 2 && e == hipSuccess) e = fork();
     if (sw) {
         if (e == hipSuccess) e = bnf_launch_decode_sw_tu7(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
         mode |= BNF_MODE_SW;
@@ -4705,6 +4933,10 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
             if (e == hipSuccess) e = ej;
         }
         lk.unlock();
+    } else if (seg_only) {
+        g_seg_launches.fetch_add(1, std::memory_order_relaxed);
+        if (e == hipSuccess)
+            e = bnf_launch_decode_seg_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, s);
     } else {
         if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, s);
         if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, s);

@@ -50,6 +50,8 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes,
                              bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
                              bnf_frame_info *info, uint32_t *order, hipEvent_t ev_crc, hipStream_t s);
+hipError_t bnf_launch_fill_bad(const bnf_frame_info *info, uint32_t nframes, bnf_stream_params sp, int fmt,
+                               uint8_t *out, uint64_t out_bytes, hipStream_t s);
 hipError_t bnf_launch_chain(const uint8_t *bytes, uint64_t nbytes, const uint64_t *cand, uint32_t ncand,
                             const bnf_frame_info *info, uint64_t first_off, bnf_stream_params sp, uint32_t *gap_crc,
                             int32_t *jump, uint32_t levels, uint32_t *mark, uint32_t *pos, uint64_t *bs, uint8_t *small,
@@ -156,6 +158,8 @@ extern "C" void bnf_set_decode_sys(int mode);
 /* k_decode_sys (systolic restore, every frame class): -1 auto (BNFLAC_DECODE_SYS), 0 the lane
  * kernels by class, 1 always (tests, A/B) */
 extern "C" BNFLAC_API void bnflac_debug_set_decode_sys(int mode) { bnf_set_decode_sys(mode); }
+extern "C" uint64_t bnf_decode_seg_launches();
+extern "C" BNFLAC_API uint64_t bnflac_debug_decode_seg_launches(void) { return bnf_decode_seg_launches(); }
 extern "C" hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset);
 /* k_parse_wave's debug counters (collected when BNFLAC_PW_STATS is set): passes, splice rounds,
  * serial fallbacks, partitions, frames, wave-cycles in scans.  out8: 8 values. */
@@ -338,6 +342,8 @@ extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d
     hipError_t e = bnf_launch_decode((const uint32_t *)d_bytes, nbytes, nframes, p,
                                      lanes_for(sp->channels), out_format, d_out, out_bytes, (bnf_frame_info *)d_info,
                                      (uint32_t *)ctx->order.p, ev, (hipStream_t)hs);
+    if (e == hipSuccess) /* a non-OK frame's range: zeros (include/bnflac.h) */
+        e = bnf_launch_fill_bad((const bnf_frame_info *)d_info, nframes, p, out_format, d_out, out_bytes, (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_decode: ") + hipGetErrorString(e));
 }
 

@@ -125,7 +125,7 @@ DECODER_SYMBOLS = [
 BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error", "bnflac_device_count",
                  "bnflac_index_frames", "bnflac_decode_frames", "bnflac_parse_frames", "bnflac_decode_parsed",
                  "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats", "bnflac_debug_set_crc_pass", "bnflac_debug_set_parse_wave", "bnflac_debug_parse_wave_stats",
-                 "bnflac_debug_set_decode_sys", "bnflac_md5_interleaved32", "bnflac_index_stream"]
+                 "bnflac_debug_set_decode_sys", "bnflac_debug_decode_seg_launches", "bnflac_md5_interleaved32", "bnflac_index_stream"]
 READER_SYMBOLS = ["bnflac_reader_open", "bnflac_reader_params", "bnflac_reader_read", "bnflac_reader_close",
                   "bnflac_reader_last_error", "bnflac_reader_seek", "bnflac_reader_read_filereader",
                   "bnflac_reader_pool_release"]
@@ -177,6 +177,7 @@ def load() -> ctypes.CDLL:
     L.bnflac_debug_set_crc_pass.argtypes = [ctypes.c_int]
     L.bnflac_debug_set_parse_wave.argtypes = [ctypes.c_int]
     L.bnflac_debug_set_decode_sys.argtypes = [ctypes.c_int]
+    L.bnflac_debug_decode_seg_launches.restype, L.bnflac_debug_decode_seg_launches.argtypes = ctypes.c_uint64, []
     L.bnflac_debug_parse_wave_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.bnflac_debug_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.bnflac_debug_stats.restype = ctypes.c_int

@@ -156,10 +156,10 @@ BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_bytes, uint
  * sample number (frame number x STREAMINFO blocksize for fixed-blocksize streams) minus
  * base_sample.  Frames that would end past out_bytes are not written (status 3,
  * flags bit 1).  d_info receives one record per frame.  A frame whose status is not OK
- * (a parse error or truncation inside a subframe: libFLAC writes nothing for it) leaves its
- * output range unspecified: the lane kernels may have stored part of it before finding the
- * error.  A CRC-16 mismatch is status OK with crc_ok 0 and a zero-filled frame, as libFLAC
- * writes it.  Asynchronous on hip_stream. */
+ * (an error or truncation inside a subframe; libFLAC writes nothing for it) has its output
+ * range zero-filled when its header parsed (sub_start[0] != 0), and is not written when the
+ * header itself failed (no range).  A CRC-16 mismatch is status OK with crc_ok 0 and a
+ * zero-filled frame, as libFLAC writes it.  Asynchronous on hip_stream. */
 BNFLAC_API int bnflac_decode_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
                                     const uint64_t *d_frame_offsets, uint32_t nframes,
                                     const bnflac_stream_params *sp, const uint64_t *d_out_sample,
@@ -195,6 +195,10 @@ BNFLAC_API void bnflac_debug_set_parse_wave(int mode);
  * (-1 auto: env BNFLAC_DECODE_SYS, else k_decode_sys for launches below 1024 subframe waves of
  * the lane kernels; 0 the lane kernels by class; 1 always); identical PCM and records. */
 BNFLAC_API void bnflac_debug_set_decode_sys(int mode);
+/* Debug: how many decodes of this process took the W16 / W32 classes through one small
+ * segment grid (k_decode_seg: the previous decode order on the device had neither class)
+ * instead of the two full-size side grids. */
+BNFLAC_API uint64_t bnflac_debug_decode_seg_launches(void);
 /* Debug: k_parse_wave's counters, collected while BNFLAC_PW_STATS is set in the environment
  * (passes, splice rounds, serial fallbacks, partitions, frames, scan / window-wait / splice
  * wave-cycles).  out8 holds 8 values; reset != 0 clears them.  0 or -1. */

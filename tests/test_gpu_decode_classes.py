@@ -7,7 +7,10 @@ instances, which never look at stereo fast-path frames.
 These tests put hand-back-prone stereo frames, LPC-12 (W16) and LPC-32 (W32) frames into
 one batch, so the decode order's 32-frame blocks mix the classes at their edges, and
 compare with the generator's source PCM and with the serial order (BNFLAC_DECODE_SERIAL=1,
-in a child process).
+in a child process).  The batches here are small enough for k_decode_sys's auto range, so the
+module pins the lane kernels.  When the previous decode order had no W16 / W32 frames, both
+classes go through one small segment grid (k_decode_seg) instead of the side grids: the last
+test decodes a batch without them first, so that its mixed batch takes that path.
 """
 import os
 import subprocess
@@ -21,6 +24,18 @@ from tests.conftest import gpu_available
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FL_REDO = 16
+
+
+@pytest.fixture(autouse=True)
+def _lane_kernels():
+    if not gpu_available():
+        yield
+        return
+    from birdnest.audio_amd import libflac
+    L = libflac.load()
+    L.bnflac_debug_set_decode_sys(0)
+    yield
+    L.bnflac_debug_set_decode_sys(-1)
 
 
 def _mixed_batch(n_each):
@@ -93,7 +108,34 @@ sys.stdout.buffer.write(out.tobytes())
 def test_side_stream_matches_other_orders(env):
     data, offs, osmp, pcm, total = _mixed_batch(20)
     out, _ = _decode(data, offs, osmp, total)
-    r = subprocess.run([sys.executable, "-c", _CHILD, ROOT], env=dict(os.environ, **env), capture_output=True,
-                       timeout=100)
+    r = subprocess.run([sys.executable, "-c", _CHILD, ROOT], env=dict(os.environ, BNFLAC_DECODE_SYS="0", **env),
+                       capture_output=True, timeout=100)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     assert r.stdout == out.tobytes()
+
+
+def _plain_c2(nframes):
+    from birdnest.audio_amd import synth
+    s = synth.encode(synth.config("C2", nframes=nframes, seed=44))
+    fo = s.frame_offsets.astype(np.int64)
+    osmp = np.arange(len(fo), dtype=np.int64) * 4096
+    return s.data.tobytes(), fo, osmp, s.pcm, s.nsamples
+
+
+@pytest.mark.skipif(not gpu_available(), reason="no GPU")
+@pytest.mark.parametrize("n_each", [7, 45])
+def test_segment_grid_after_batch_without_w16_w32(n_each):
+    from birdnest.audio_amd import libflac
+    L = libflac.load()
+    data, offs, osmp, pcm, total = _plain_c2(40)
+    out, info = _decode(data, offs, osmp, total)  # records W16 = W32 = 0 for the next decode
+    assert np.array_equal(out.view("<i4").reshape(-1, 2), pcm)
+    data, offs, osmp, pcm, total = _mixed_batch(n_each)
+    n0 = L.bnflac_debug_decode_seg_launches()
+    out, info = _decode(data, offs, osmp, total)  # W16 + W32 through k_decode_seg
+    assert L.bnflac_debug_decode_seg_launches() == n0 + 1
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    assert np.array_equal(out.view("<i4").reshape(-1, 2), pcm)
+    out2, info2 = _decode(data, offs, osmp, total)  # this batch had both: the side grids again
+    assert L.bnflac_debug_decode_seg_launches() == n0 + 1
+    assert out2.tobytes() == out.tobytes() and info2.tobytes() == info.tobytes()

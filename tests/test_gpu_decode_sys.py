@@ -4,8 +4,8 @@ lane kernels (k_decode_st, k_decode_sw, k_decode<W>), which the rest of the suit
 the oracle: identical records and identical PCM for every frame that decodes (status OK,
 CRC-failed frames zero-filled in both).  Frames k_decode_sys hands back (errors, truncation, an
 MMX16 subframe leaving int16, a 64-bit shift >= 32) go through k_decode_list, the exact lane
-kernel, so their records are the lane path's too.  A frame that ends TRUNC / ERROR has
-unspecified PCM in both paths (include/bnflac.h) and is not compared byte for byte."""
+kernel, so their records are the lane path's too.  A frame that ends TRUNC / ERROR has its range
+zero-filled by k_fill_bad in both paths (include/bnflac.h), so the whole output buffer must match."""
 import json
 import os
 
@@ -90,6 +90,11 @@ def _same(gpu, data, offs, fmt):
         s0, nb = _frame_range(libflac, fmt, a, i, stride)
         assert np.array_equal(oa[s0:s0 + nb], ob[s0:s0 + nb]), f"PCM of frame {i} (offset {offs[i]}) differs"
         n += 1
+    for i in np.nonzero((a["status"] == 1) | (a["status"] == 2))[0]:  # k_fill_bad: zeros, or untouched
+        s0, nb = _frame_range(libflac, fmt, a, i, stride)
+        if a["sub_start"][i][0] != 0 and s0 + nb <= len(oa) - 64:
+            assert not oa[s0:s0 + nb].any(), f"non-OK frame {i} (offset {offs[i]}) not zero-filled"
+    assert oa.tobytes() == ob.tobytes()
     return n, b
 
 

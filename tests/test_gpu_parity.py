@@ -1000,3 +1000,43 @@ def test_ring_crc_damage_positions(gpu, cfg, kw):
             bs = int(info["blocksize"][f])
             assert not out.view("<i2")[f * bs * 2:(f + 1) * bs * 2].any()
     assert bad >= len(pos) - 2  # a flipped bit is (almost always) caught
+
+
+@pytest.mark.parametrize("decode_mode", [0, 2], indirect=True)
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_non_ok_frame_range_zero_filled(gpu, cfg, decode_mode):
+    """The batch API's output for a frame that does not decode (include/bnflac.h): the last
+    frame cut short inside its subframes (status TRUNC, header parsed) leaves zeros over its
+    whole range, not the lane kernels' partial stores; a frame whose header fails (a broken
+    sync code) leaves its range untouched; the other frames decode bit-exactly."""
+    from birdnest.audio_amd import synth
+    torch, libflac, dec = gpu
+    s = synth.encode(synth.config(cfg, nframes=6, last_blocksize=0))
+    data = bytearray(s.data.tobytes())
+    offs = [int(o) for o in s.frame_offsets]
+    data[offs[2] + 1] ^= 0x02  # frame 2: 0xFFF8 -> 0xFFFA, a header error (reserved bit)
+    sp = _stream_params(libflac, bytes(data))
+    fmt = libflac.OUT_INTERLEAVED32
+    stride = libflac.out_stride(fmt, sp)
+    dev = torch.device("cuda:0")
+    cut = offs[5] + (len(data) - offs[5]) // 2  # frame 5 ends past nbytes
+    d_bytes = torch.zeros((len(data) + 3) // 4 * 4 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    d_offs = torch.tensor(offs, dtype=torch.int64, device=dev)
+    d_os = torch.tensor([i * sp.max_blocksize for i in range(6)], dtype=torch.int64, device=dev)
+    d_out = torch.full((sp.total_samples * stride,), 0xAB, dtype=torch.uint8, device=dev)
+    d_info = torch.zeros(6 * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    dec.decode_frames(d_bytes, cut, d_offs, 6, sp, fmt, d_out, d_info, d_out_sample=d_os)
+    torch.cuda.synchronize()
+    info = libflac.info_array(d_info.cpu().numpy())
+    out = d_out.cpu().numpy()
+    bs = sp.max_blocksize * stride
+    assert info["status"][5] == 2 and info["sub_start"][5][0] != 0
+    assert not out[5 * bs:6 * bs].any()
+    assert info["status"][2] == 1 and info["sub_start"][2][0] == 0
+    assert (out[2 * bs:3 * bs] == 0xAB).all()
+    pcm = out.view("<i4").reshape(-1, sp.channels)
+    for i in (0, 1, 3, 4):
+        assert info["status"][i] == 0 and info["crc_ok"][i] == 1
+        n = sp.max_blocksize
+        assert np.array_equal(pcm[i * n:(i + 1) * n], s.pcm[i * n:(i + 1) * n])
