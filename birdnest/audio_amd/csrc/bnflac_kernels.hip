@@ -3945,19 +3945,33 @@ DEV void sw_line_group(lds_u32x4 *stg, uint32_t lane, bool odd, bool carry, SwLn
         q.h1 = u0; q.h2 = u1; q.h3 = u2;
     }
 }
-/* every lane active: the slots' line of each frame to base(frame) (0: not stored); returns
- * the store instructions issued */
-DEV uint32_t sw_line_flush(const lds_u32x4 *stg, uint64_t base, uint32_t lane) {
+/* The run base and blocksize of frame (lane >> 2) + 16 i (0 for a frame that is not
+ * decoded), fetched once per wave by ds_bpermute with every lane active */
+struct SwRuns {
+    uint64_t a[4];
+    uint32_t bs[4];
+};
+DEV void sw_runs(SwRuns &r, uint64_t run, uint32_t bs, uint32_t lane) {
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        const int src = (int)(((lane >> 2) + 16u * i) << 2);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)run);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(run >> 32));
+        r.a[i] = ((uint64_t)hi << 32) | lo;
+        r.bs[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(run ? bs : 0u));
+    }
+}
+/* every lane active: the slots' line at byte `off` of the chunk's frames (those whose run
+ * reaches sample n0 + 16); returns the store instructions issued */
+DEV uint32_t sw_line_flush(const lds_u32x4 *stg, const SwRuns &r, uint32_t n0, int32_t off, uint32_t lane) {
     uint32_t n = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 4; i++) {
         const uint32_t src = (lane >> 2) + 16u * i;
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)base);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)(base >> 32));
-        const uint64_t a = ((uint64_t)hi << 32) | lo;
+        const bool on = n0 + ST_CHK <= r.bs[i];
         const u32x4 v = stg[src * 4u + (lane & 3u)];
-        if (a) gst128(a + 16u * (lane & 3u), v);
-        if (any_lane(a != 0)) n++;
+        if (on) gst128(r.a[i] + (uint64_t)((int64_t)n0 * 6 + off) + 16u * (lane & 3u), v);
+        if (any_lane(on)) n++;
     }
     return n;
 }
@@ -4163,6 +4177,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     lds_u32x4 *stg = (lds_u32x4 *)((lds_u32 *)ring + 2u * ST_RD * RING_LANE_DW);
     static_assert(sizeof(ring) >= (2u * ST_RD * RING_LANE_DW + 1024u) * 4u, "line slots past the rings");
     SwLn q;
+    SwRuns runs;
+    if (line) sw_runs(runs, ok ? (uint64_t)(uintptr_t)dst : 0ull, bs, lane);
     bool carry = false, cvalid = false; /* carry: an even chunk left its half line (wave-uniform) */
     uint32_t carry_b = 0;                /* its byte offset in the runs */
     wait_vm(); /* setup loads done: the store count starts from zero */
@@ -4228,18 +4244,17 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
                 z1.left -= ST_CHK;
             }
             if (ln) { /* every lane active: the chunk's lines (sw_line_flush) */
-                const uint64_t run = valid ? (uint64_t)(uintptr_t)dst + (uint64_t)n0 * 6u : 0ull;
                 if (!odd) {
-                    nst += sw_line_flush(stg, run, lane);
+                    nst += sw_line_flush(stg, runs, n0, 0, lane);
                     carry = true;
                     cvalid = valid;
                     carry_b = n0 * 6u + 64u; /* units c0, c1: bytes 64..95 of the chunk */
                 } else {
                     if (!carry) nst += 2u; /* the direct half line (sw_line_group) */
-                    if (carry) nst += sw_line_flush(stg, run ? run - 32u : 0ull, lane);
+                    if (carry) nst += sw_line_flush(stg, runs, n0, -32, lane);
                     lds_u32x4 *my = stg + lane * 4u;
                     my[0] = q.h0; my[1] = q.h1; my[2] = q.h2; my[3] = q.h3;
-                    nst += sw_line_flush(stg, run ? run + 32u : 0ull, lane);
+                    nst += sw_line_flush(stg, runs, n0, 32, lane);
                     carry = false;
                 }
             } else if (all_al && sto && any_lane(valid)) {
