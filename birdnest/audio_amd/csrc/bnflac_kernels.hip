@@ -803,6 +803,39 @@ DEV void skip_step(BR &b, uint32_t &rem, uint32_t k, uint32_t k1, uint32_t km, u
     }
 }
 
+/* skip_step without its own slow-path test: a lane whose first codeword does not fit its
+ * window (`stall`) advances nothing, so it stalls again in the next step on the same window;
+ * the caller tests the pair's stalls once (skip_stall) */
+DEV void skip_step_ns(BR &b, uint32_t &rem, uint32_t k1, uint32_t km, bool &stall) {
+    const bool live = rem != 0u;
+    const uint32_t w = br_peek(b);
+    const uint32_t q1 = min(ffbh_b(w), 32u);
+    const bool fit1 = live & (q1 <= km);
+    const uint32_t len1 = q1 + k1;
+    const uint32_t q2 = min(ffbh_b(w << (len1 & 31u)), 32u);
+    const uint32_t len2 = len1 + q2 + k1;
+    const bool fit2 = fit1 & (rem >= 2u) & (len2 <= 32u);
+    stall = stall | (live & !fit1);
+    br_adv(b, fit2 ? len2 : (fit1 ? len1 : 0u));
+    rem -= fit2 ? 2u : (fit1 ? 1u : 0u); /* fit2 implies fit1 */
+}
+DEV void skip_stall(BR &b, uint32_t &rem, uint32_t k, uint32_t &p, uint32_t parts, bool &tr, uint64_t limit, bool &stall) {
+    if (__builtin_expect(any_lane(stall), 0)) {
+        if (stall) { /* a unary prefix too long for the window */
+            uint32_t qq;
+            if (br_unary(b, qq, limit)) {
+                br_adv(b, k);
+                rem--;
+            } else { /* truncated: this lane stops walking */
+                tr = true;
+                rem = 0;
+                p = parts;
+            }
+        }
+        stall = false;
+    }
+}
+
 /* Skip the residual of a FIXED/LPC subframe (k_parse's cursor walk).  One loop over the
  * subframe's codewords: a lane whose partition is done reads the next partition header
  * (and skips escaped partitions) on a rare path inside the same loop, so lanes whose
@@ -844,9 +877,19 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
             }
         }
         /* two steps per switch test (a lane that finishes its partition in the first one
-         * idles in the second) */
-        skip_step(b, rem, k, k1, km, p, parts, tr, limit);
-        skip_step(b, rem, k, k1, km, p, parts, tr, limit);
+         * idles in the second) and per slow-path test */
+#ifndef BNF_PARSE_NS
+#define BNF_PARSE_NS 1
+#endif
+        if (BNF_PARSE_NS) {
+            bool stall = false;
+            skip_step_ns(b, rem, k1, km, stall);
+            skip_step_ns(b, rem, k1, km, stall);
+            skip_stall(b, rem, k, p, parts, tr, limit, stall);
+        } else {
+            skip_step(b, rem, k, k1, km, p, parts, tr, limit);
+            skip_step(b, rem, k, k1, km, p, parts, tr, limit);
+        }
     }
     return (tr || br_pos(b) > limit) ? BNF_ST_TRUNC : BNF_ST_OK;
 }
