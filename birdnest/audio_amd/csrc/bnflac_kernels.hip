@@ -4887,8 +4887,12 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
                            out_sample_in, base_sample, info, pws, seg);
         return hipGetLastError();
     }
+    /* the parse order (walk length from the header bytes): a fixed-blocksize stream's frames
+     * all walk the same length (the last one aside), so the order only costs its three
+     * launches there (C2: 0.12 ms per 1,024 batches) */
     const uint32_t *perm = nullptr;
-    if (order) {
+    const bool fixed_bs = sp.has_stream_info && sp.min_blocksize == sp.max_blocksize;
+    if (order && !fixed_bs) {
         hipError_t e = launch_order<1>(nullptr, (const uint8_t *)words, nbytes, frame_offs, nframes, order, &perm, s);
         if (e != hipSuccess) return e;
     }
