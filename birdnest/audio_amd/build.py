@@ -43,6 +43,23 @@ def hipcc():
 KERNEL_TUS = (0, 1, 2, 3, 4, 5, 7)  # one build of bnflac_kernels.hip per BNF_TU: scan+parse, k_decode<8>, k_decode<32> + k_decode_list, k_decode_st<FLACDECODER>, k_decode_st<others>, k_decode<16>, k_decode_sw (TU 8: bnflac_sys.hip)
 
 
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden"]
+
+
+def source_hash() -> str:
+    """Hash of everything libbnflac.so is built from: every HIP/C++ source and header, the
+    kernel TU split and the hipcc flags.  bench.py stamps its line with it, and a committed PMC
+    summary (profiles/traffic_*.json) is attached to a bench run only when the stamps match."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in HIP_SOURCES + HIP_HEADERS:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(repr((KERNEL_TUS, HIPCC_FLAGS)).encode())
+    return h.hexdigest()[:16]
+
+
 def build_hip(force=False, verbose=False):
     """Compile the kernel TUs and the runtime in parallel (hipcc -c), then link.
 
@@ -56,7 +73,7 @@ def build_hip(force=False, verbose=False):
         os.makedirs(libdir, exist_ok=True)
         objdir = os.path.join(vdir, "build") if vdir else os.path.join(PKG, "build")
         os.makedirs(objdir, exist_ok=True)
-        base = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-I" + INCLUDE]
+        base = [hipcc()] + HIPCC_FLAGS + ["-I" + INCLUDE]
         if vdir:
             base += os.environ.get("BNFLAC_EXTRA_CFLAGS", "").split()
         jobs, objs = [], []

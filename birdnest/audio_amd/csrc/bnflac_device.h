@@ -37,15 +37,8 @@ typedef struct {
     uint32_t crc_ok;
     uint32_t sub_start[8];  /* bit offset of each subframe header, relative to frame_off*8 */
     uint32_t flags;         /* BNF_FL_* */
-    uint32_t crc_next;      /* BNF_CN_*: CRC-16 of [frame_off, next frame's offset), from the coalesced
-                               CRC pass fused into k_parse's launch; 0 when not computed */
+    uint32_t reserved;      /* 0 (the 128-byte record's last word) */
 } bnf_frame_info;
-
-/* crc_next: a frame whose footer ends exactly at frame_off + (crc_next & BNF_CN_LEN) passed
- * its CRC-16 check iff BNF_CN_ZERO is set (the CRC of a whole frame, footer included, is 0) */
-#define BNF_CN_VALID 0x80000000u
-#define BNF_CN_ZERO 0x40000000u
-#define BNF_CN_LEN 0x3FFFFFFFu
 
 enum {
     BNF_FL_NEEDS_SLOW = 1u,
@@ -55,7 +48,6 @@ enum {
     BNF_FL_ST = 32u,           /* set by k_parse: 2-channel frame, LPC orders <= 8 (k_decode_st's candidates) */
     BNF_FL_REDO = 64u,         /* set by k_decode_st: declined (rare case), decoded again by k_decode<8> */
     BNF_FL_W16 = 128u,         /* set by k_parse: LPC orders 9..16, or LPC above 16 bits (k_decode<16>) */
-    BNF_FL_CRC_DEFER = 256u,   /* decoded with the CRC-16 check left to k_crc_join (concurrent CRC pass) */
     BNF_FL_WAVE_REDO = 512u,   /* set by k_decode_sys: handed back, decoded again by k_decode_list */
     BNF_FL_SW = 1024u          /* set by k_parse: 2-channel W16 frame of 17..24 bits, LPC orders <= 12 (k_decode_sw's candidates) */
 };

@@ -101,11 +101,8 @@ typedef __attribute__((address_space(1))) const void gvoid;
  * lgkmcnt -- every later LDS wait would then wait for the HBM write) */
 DEV void gst128(uint64_t addr, u32x4 v) { *(__attribute__((address_space(1))) u32x4 *)addr = v; }
 
-/* Mode bit carried in the kernels' `ablate` word (set by the launchers, never a timing
- * ablation): the decode kernels leave the CRC-16 check to k_crc_join, because the
- * concurrent CRC pass (k_crc, on a second stream) is still running. */
-#define BNF_MODE_DEFER_CRC 0x1000u
-/* Mode bit: the lane kernel decodes only the frames k_decode_sys handed back (BNF_FL_WAVE_REDO). */
+/* Mode bits carried in the kernels' `ablate` word (set by the launchers, never a timing
+ * ablation).  Mode bit: the lane kernel decodes only the frames k_decode_sys handed back (BNF_FL_WAVE_REDO). */
 #define BNF_MODE_WREDO 0x4000u
 /* Mode bit: k_decode_sw ran before the other lane kernels (they take its SW frames only when
  * it handed them back).  Host ablation bit BNF_ABLATE_NO_SW: do not launch it. */
@@ -774,36 +771,8 @@ DEV uint32_t parse_subframe_head(R &b, uint32_t bps, uint32_t bs, uint64_t limit
  * an exec-masked region per step), and the leading-zero counts use the builtin form (the
  * asm one costs a wait state after each), ~30 VALU per step instead of ~55 (round 4). */
 DEV uint32_t ffbh_b(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : ~0u; }
-DEV void skip_step(BR &b, uint32_t &rem, uint32_t k, uint32_t k1, uint32_t km, uint32_t &p, uint32_t parts, bool &tr,
-                   uint64_t limit) {
-    const bool live = rem != 0u;
-    const uint32_t w = br_peek(b);
-    const uint32_t q1 = min(ffbh_b(w), 32u); /* 32 for an empty window: no fit */
-    const bool fit1 = q1 <= km;
-    const uint32_t len1 = q1 + k1;
-    const uint32_t q2 = min(ffbh_b(w << (len1 & 31u)), 32u);
-    const uint32_t len2 = len1 + q2 + k1; /* both codewords: fits iff <= 32 (and the first fits) */
-    const bool fit2 = fit1 & (rem >= 2u) & (len2 <= 32u);
-    const bool slow1 = live & !fit1;
-    const bool slow = any_lane(slow1);
-    br_adv(b, live ? (fit2 ? len2 : (fit1 ? len1 : 0u)) : 0u);
-    rem -= live ? (fit2 ? 2u : (uint32_t)fit1) : 0u;
-    if (__builtin_expect(slow, 0)) {
-        if (slow1) { /* a unary prefix too long for the window */
-            uint32_t qq;
-            if (br_unary(b, qq, limit)) {
-                br_adv(b, k);
-                rem--;
-            } else { /* truncated: this lane stops walking */
-                tr = true;
-                rem = 0;
-                p = parts;
-            }
-        }
-    }
-}
 
-/* skip_step without its own slow-path test: a lane whose first codeword does not fit its
+/* The step has no slow-path test of its own: a lane whose first codeword does not fit its
  * window (`stall`) advances nothing, so it stalls again in the next step on the same window;
  * the caller tests the pair's stalls once (skip_stall) */
 DEV void skip_step_ns(BR &b, uint32_t &rem, uint32_t k1, uint32_t km, bool &stall) {
@@ -878,17 +847,11 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
         }
         /* two steps per switch test (a lane that finishes its partition in the first one
          * idles in the second) and per slow-path test */
-#ifndef BNF_PARSE_NS
-#define BNF_PARSE_NS 1
-#endif
-        if (BNF_PARSE_NS) {
+        {
             bool stall = false;
             skip_step_ns(b, rem, k1, km, stall);
             skip_step_ns(b, rem, k1, km, stall);
             skip_stall(b, rem, k, p, parts, tr, limit, stall);
-        } else {
-            skip_step(b, rem, k, k1, km, p, parts, tr, limit);
-            skip_step(b, rem, k, k1, km, p, parts, tr, limit);
         }
     }
     return (tr || br_pos(b) > limit) ? BNF_ST_TRUNC : BNF_ST_OK;
@@ -1283,16 +1246,13 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 }
 
 /* ==================================================================== k_parse */
-#ifndef PARSE_RD
 #define PARSE_RD 8 /* ring slots per lane (8 KB of LDS per wave, 5 waves per SIMD); 4 slots: 8 waves but 3% slower */
-#endif
 /* One lane per candidate frame: header + cursor walk over subframes 0..C-2.  Also
- * flags frames with an LPC order above 8 (they go to k_decode<32>).  keep_cn: the CRC pass
- * of the same launch owns the record's crc_next word (not written here). */
+ * flags frames with an LPC order above 8 (they go to k_decode<32>). */
 DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const uint64_t *__restrict__ frame_offs,
                      uint32_t nframes, const bnf_stream_params &sp, const uint64_t *__restrict__ out_sample_in,
                      uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate, lds_u32 *ring,
-                     uint32_t f, bool keep_cn) {
+                     uint32_t f) {
     if (f >= nframes) return;
     bnf_frame_info fi;
     fi.status = BNF_ST_OK;
@@ -1307,7 +1267,7 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
     fi.out_sample = 0;
     fi.crc8 = fi.crc16_calc = fi.crc16_read = fi.crc_ok = 0;
     fi.flags = 0;
-    fi.crc_next = 0;
+    fi.reserved = 0;
     /* sub_start is kept in registers and written by select chains: indexing fi.sub_start
      * with the runtime channel would put the whole record in scratch */
     uint32_t ss[8];
@@ -1375,14 +1335,7 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
     fi.status = st;
 #pragma unroll
     for (int c = 0; c < 8; c++) fi.sub_start[c] = ss[c];
-    if (keep_cn) { /* every word but crc_next (written concurrently by the CRC pass) */
-        const uint32_t *src = (const uint32_t *)&fi;
-        uint32_t *dst = (uint32_t *)&info[f];
-#pragma unroll
-        for (int i = 0; i < 31; i++) dst[i] = src[i];
-    } else {
-        info[f] = fi;
-    }
+    info[f] = fi;
 }
 
 #endif /* BNF_TU == 0 */
@@ -1698,61 +1651,18 @@ DEV void crc_tk_fill(lds_u16 *TK, uint32_t lane) {
 }
 
 #if BNF_TU == 0
-/* ============================================================== k_parse launch
- * One launch, two kinds of single-wave workgroups, interleaved by block index:
- *  - parse blocks: parse_frame, one lane per frame (lane-serial subframe walk);
- *  - CRC blocks: one wave per frame, CRC_FPW consecutive frames each: the CRC-16 of
- *    [offset f, offset f+1) (read_frame_'s footer check @0x10011a01 for a frame that ends
- *    where the next one starts) over coalesced 1 KB wave loads.
- * The walk is latency-bound and the CRC pass streams, so they share the chip; the decode
- * kernels then skip their own lane-scattered CRC re-read (crc_next, BNF_CN_*).
- * CRC layout: 16-byte pieces counted back from e = round_up(b1, 16); lane l takes pieces
- * 63 - l + 64 m, so every wave load is 64 consecutive pieces.  Each lane runs a CRC over
- * its own pieces with the 1008 bytes between them as zeros (x^(8*1008) by table), shifts
- * the result to e (x^(8*16*(63 - l))), and the lanes are XOR-reduced: the CRC of the range
- * times x^(8(e - b1)), which is 0 iff the range's CRC is 0 (x is invertible mod P).  Bytes
- * outside [b0, b1) are masked to 0 (leading zeros leave a zero-initialised CRC at 0). */
-#define CRC_FPW 16
-
-DEV void crc_frames(const uint8_t *__restrict__ bytes, uint64_t nbytes, const uint64_t *__restrict__ offs,
-                    uint32_t nframes, uint32_t f0, bnf_frame_info *__restrict__ info, const lds_u16 *T,
-                    const lds_u16 *TK, uint32_t lanec, uint32_t lane) {
-    const uint32_t fe = min(f0 + CRC_FPW, nframes);
-    for (uint32_t f = f0; f < fe; f++) {
-        const uint64_t b0 = offs[f];
-        const uint64_t b1 = f + 1u < nframes ? offs[f + 1u] : 0ull;
-        uint32_t word = 0;
-        if (b1 > b0 && b1 <= nbytes && b1 - b0 <= BNF_CN_LEN) { /* wave-uniform */
-            const uint32_t acc = wave_crc_range(bytes, b0, b1, T, TK, lanec, lane);
-            word = BNF_CN_VALID | (acc == 0u ? BNF_CN_ZERO : 0u) | (uint32_t)(b1 - b0);
-        }
-        if (lane == 0) info[f].crc_next = word;
-    }
-}
-
+/* ============================================================== k_parse
+ * One lane per frame (parse_frame: the lane-serial subframe walk), 64 frames per single-wave
+ * workgroup, in the parse order when there is one. */
 __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint64_t nbytes,
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
                                               uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate,
-                                              uint32_t nparse, uint32_t ncrc, const uint32_t *__restrict__ perm,
-                                              uint32_t keep_cn) {
-    __shared__ LDS_DMA_ALIGN uint32_t ring[PARSE_RD * RING_LANE_DW]; /* parse: the bit ring; CRC: the tables */
-    static_assert(PARSE_RD * RING_LANE_DW * 4 >= (8 * 256 + 512) * 2, "CRC tables fit the ring");
-    const uint32_t lane = threadIdx.x;
-    const uint32_t tot = nparse + ncrc, b = blockIdx.x;
-    const uint32_t pb = (uint32_t)((uint64_t)b * nparse / tot), pb1 = (uint32_t)((uint64_t)(b + 1u) * nparse / tot);
-    if (pb1 > pb) {
-        const uint32_t slot = pb * 64u + lane; /* parse order (launch_order<1>) */
-        parse_frame(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
-                    (perm && slot < nframes) ? perm[slot] : slot, ncrc != 0 || keep_cn != 0);
-        return;
-    }
-    lds_u16 *T = (lds_u16 *)(lds_u32 *)ring, *TK = T + 8 * 256;
-    for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
-    crc_tk_fill(TK, lane); /* x^(8*1008) mod P by bytes */
-    const uint32_t lanec = crc16_shift(1u, 16u * (63u - lane));
-    __syncthreads();
-    crc_frames((const uint8_t *)words, nbytes, frame_offs, nframes, (b - pb) * CRC_FPW, info, T, TK, lanec, lane);
+                                              const uint32_t *__restrict__ perm) {
+    __shared__ LDS_DMA_ALIGN uint32_t ring[PARSE_RD * RING_LANE_DW]; /* the bit ring */
+    const uint32_t slot = blockIdx.x * 64u + threadIdx.x; /* parse order (launch_order<1>) */
+    parse_frame(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
+                (perm && slot < nframes) ? perm[slot] : slot);
 }
 
 /* =========================================================== k_parse_wave
@@ -1783,7 +1693,7 @@ __global__ void __launch_bounds__(64) k_parse_wave(const uint32_t *__restrict__ 
     fi.out_sample = 0;
     fi.crc8 = fi.crc16_calc = fi.crc16_read = fi.crc_ok = 0;
     fi.flags = 0;
-    fi.crc_next = 0;
+    fi.reserved = 0;
     uint32_t ss[8];
 #pragma unroll
     for (int c = 0; c < 8; c++) ss[c] = 0;
@@ -1854,62 +1764,6 @@ __global__ void __launch_bounds__(64) k_parse_wave(const uint32_t *__restrict__ 
     if (lane < 32u) ((uint32_t *)&info[f])[lane] = v;
 }
 
-/* The same CRC pass as its own kernel, for a second stream: it runs beside k_parse and the
- * decode kernels (it streams coalesced 1 KB loads; they are bound by lane-scattered memory
- * requests), which then defer the check to k_crc_join. */
-__global__ void __launch_bounds__(64) k_crc(const uint32_t *__restrict__ words, uint64_t nbytes,
-                                            const uint64_t *__restrict__ frame_offs, uint32_t nframes,
-                                            bnf_frame_info *__restrict__ info) {
-    __shared__ uint32_t tabs[(8 * 256 + 512) / 2];
-    const uint32_t lane = threadIdx.x;
-    lds_u16 *T = (lds_u16 *)(lds_u32 *)tabs, *TK = T + 8 * 256;
-    for (uint32_t i = lane; i < 8u * 256u; i += 64u) T[i] = (&g_crc16_tab[0][0])[i];
-    crc_tk_fill(TK, lane); /* x^(8*1008) mod P by bytes */
-    const uint32_t lanec = crc16_shift(1u, 16u * (63u - lane));
-    __syncthreads();
-    crc_frames((const uint8_t *)words, nbytes, frame_offs, nframes, blockIdx.x * CRC_FPW, info, T, TK, lanec, lane);
-}
-
-/* After the decode kernels and k_crc: the CRC-16 verdict of every deferred frame.  A frame
- * whose footer ends where the next offset starts has its verdict in crc_next; any other
- * (the last frame of a call, a gap before the next offset) is checked here, one thread per
- * frame.  A mismatch zero-fills the frame's output, as libFLAC does (@0x10011af5) and as
- * the decode kernels' own tail would have. */
-__global__ void __launch_bounds__(256) k_crc_join(const uint8_t *__restrict__ bytes, uint32_t nframes,
-                                                  bnf_stream_params sp, int fmt, uint8_t *__restrict__ out,
-                                                  bnf_frame_info *__restrict__ info) {
-    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
-    if (f >= nframes) return;
-    const uint32_t flags = info[f].flags;
-    if (info[f].status != BNF_ST_OK || !(flags & BNF_FL_CRC_DEFER)) return;
-    const uint64_t f_off = info[f].frame_off, end_byte = (info[f].resume_bit >> 3) - 2u; /* the footer's first byte */
-    const uint32_t rd = info[f].crc16_read, cn = info[f].crc_next;
-    uint32_t calc = rd;
-    if (!((cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && f_off + (cn & BNF_CN_LEN) == end_byte + 2u)) {
-        uint32_t c = 0;
-        for (uint64_t p = f_off; p < end_byte; p++) c = ((c << 8) ^ g_crc16_tab[0][((c >> 8) ^ bytes[p]) & 0xffu]) & 0xffffu;
-        calc = c;
-    }
-    info[f].crc16_calc = calc;
-    info[f].crc_ok = calc == rd ? 1u : 0u;
-    info[f].flags = flags & ~(uint32_t)BNF_FL_CRC_DEFER;
-    if (calc != rd) {
-        const uint32_t C = info[f].channels, bsz = info[f].blocksize;
-        const uint64_t os = info[f].out_sample;
-        uint64_t start, n;
-        switch (fmt) {
-        case BNF_OUT_PLANAR32: start = os * sp.channels * 4u; n = (uint64_t)C * bsz * 4u; break;
-        case BNF_OUT_INTERLEAVED32: start = os * sp.channels * 4u; n = (uint64_t)sp.channels * bsz * 4u; break;
-        case BNF_OUT_FLACDECODER: start = os * (C == 2 ? 4u : 2u); n = (uint64_t)bsz * (C == 2 ? 4u : 2u); break;
-        default: {
-            const uint32_t fb = sp.bps == 24 ? 3u : 2u;
-            start = os * sp.channels * fb;
-            n = (uint64_t)bsz * sp.channels * fb;
-        }
-        }
-        for (uint64_t i = 0; i < n; i++) out[start + i] = 0;
-    }
-}
 
 /* The batch API's defined output for a frame whose status is not OK (bnflac_decode_parsed):
  * after every decode kernel, the output range of each ERROR / TRUNC frame whose header
@@ -1930,7 +1784,9 @@ __global__ void __launch_bounds__(64) k_fill_bad(const bnf_frame_info *__restric
             const uint32_t C = info[f].channels, bsz = info[f].blocksize;
             const uint64_t os = info[f].out_sample;
             switch (fmt) {
-            case BNF_OUT_PLANAR32: start = os * sp.channels * 4u; n = (uint64_t)C * bsz * 4u; break;
+            /* the frame's own slot only: a planar frame with more channels than sp.channels
+             * would reach into the next frame's slot, so the fill stops at sp.channels */
+            case BNF_OUT_PLANAR32: start = os * sp.channels * 4u; n = (uint64_t)min(C, sp.channels) * bsz * 4u; break;
             case BNF_OUT_INTERLEAVED32: start = os * sp.channels * 4u; n = (uint64_t)sp.channels * bsz * 4u; break;
             case BNF_OUT_FLACDECODER: start = os * (C == 2 ? 4u : 2u); n = (uint64_t)bsz * (C == 2 ? 4u : 2u); break;
             default: {
@@ -2508,7 +2364,7 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
 
     /* ---- last subframe end, zero padding, CRC-16 (read_frame_ @0x100118c0 tail).  The
      * frame record is re-read here (only scalars stay live across the chunk loop). */
-    if (lane < fpb) { t_ok[lane] = 0; t_bad[lane] = 0; t_endbit[lane] = 0; t_pre[lane] = 0; }
+    if (lane < fpb) { t_ok[lane] = 0; t_bad[lane] = 0; t_endbit[lane] = 0; }
     lds_sync();
     if (have && ch == 0) {
         t_ok[fl] = fok ? 1u : 0u;
@@ -2556,26 +2412,17 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
                     t_crc_read = crc_read;
                     t_resume = br_pos(b);
                     t_resume_set = true;
-                    /* the k_parse launch's CRC pass found this frame's CRC-16 zero; or the
-                     * concurrent pass will be checked by k_crc_join */
-                    if (ablate & BNF_MODE_DEFER_CRC) {
-                        t_pre[fl] = 1u;
-                    } else {
-                        const uint32_t cn = info[f].crc_next;
-                        if ((cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && f_off + (cn & BNF_CN_LEN) == end_byte + 2u)
-                            t_pre[fl] = 1u;
-                    }
                 }
             }
         }
         if (t_status != BNF_ST_OK) t_bad[fl] = 1;
     }
     lds_sync();
-    /* CRC-16 over [frame_off, end) for frames the CRC pass did not vouch for: split across
+    /* CRC-16 over [frame_off, end): split across
      * the frame's channel lanes, combined by polynomial shifts (CRC is linear:
      * crc(A|B) = crc(A)*x^(8|B|) + crc(B)). */
     uint32_t part = 0;
-    const bool crc_lane = fok && frame_ok && ch < fch && !t_bad[fl] && !t_pre[fl];
+    const bool crc_lane = fok && frame_ok && ch < fch && !t_bad[fl];
     lds_u16 *T = (lds_u16 *)(lds_u32 *)lds;
     if (__any(crc_lane)) { /* the rows are free now: stage the slice-by-8 CRC tables there */
         __syncthreads();
@@ -2595,29 +2442,19 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
     /* xor-reduce within each frame's lane group */
     uint32_t acc = part;
     for (uint32_t o = 1; o < chn_lanes; o <<= 1) acc ^= __shfl_xor(acc, o);
-    if (((ablate & 1u) || t_pre[fl]) && last && t_status == BNF_ST_OK) acc = t_crc_read;
+    if ((ablate & 1u) && last && t_status == BNF_ST_OK) acc = t_crc_read;
     if (last) {
         bnf_frame_info fo = info[f];
         fo.status = t_status;
         if (t_status == BNF_ST_ERROR) fo.err = t_err;
         if (t_resume_set) fo.resume_bit = t_resume;
-        if (t_status == BNF_ST_OK && (ablate & BNF_MODE_DEFER_CRC)) {
-            fo.crc16_read = t_crc_read;
-            fo.crc16_calc = 0;
-            fo.crc_ok = 0;
-            fo.flags |= BNF_FL_CRC_DEFER; /* k_crc_join decides (and zero-fills) */
-        } else if (t_status == BNF_ST_OK) {
+        if (t_status == BNF_ST_OK) {
             fo.crc16_read = t_crc_read;
             fo.crc16_calc = acc;
             fo.crc_ok = (acc == t_crc_read) ? 1u : 0u;
             if (!fo.crc_ok) t_bad[fl] = 2; /* libFLAC zero-fills a CRC-failed frame (@0x10011af5) */
         }
-        { /* every word but crc_next, which the concurrent CRC pass may be writing */
-            const uint32_t *src = (const uint32_t *)&fo;
-            uint32_t *dst = (uint32_t *)&info[f];
-#pragma unroll
-            for (int i = 0; i < 31; i++) dst[i] = src[i];
-        }
+        info[f] = fo;
     }
     __syncthreads();
     if (tmon && lane == 0) {
@@ -2924,9 +2761,6 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  * mismatch, out-of-range samples, unsupported layouts) get BNF_FL_REDO and are decoded
  * again, exactly, by k_decode<8>, which runs after it on the same stream. */
 #define ST_CHK 16 /* samples per chunk (one 64-byte FLACDecoder run per frame) */
-#ifndef BNF_ST_PAIR
-#define BNF_ST_PAIR 1 /* fused chunks decode Rice codewords two per window (st_fused_pair) */
-#endif
 #define ST_RD 8  /* 16-byte ring slots per lane and channel: two 64-byte groups */
 
 struct StCh {
@@ -3227,9 +3061,7 @@ DEV void st_refill_issue(BR &b, bool want) {
 DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line offset o: bytes below h cleared */
     return h <= o ? ~0u : (h >= o + 4u ? 0u : (~0u << (8u * (h - o))));
 }
-#ifndef CRC_LINES
 #define CRC_LINES 4
-#endif
 DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
     const lds_u16 *Tb = T + CRC11_BYTE;
     uint32_t crc = 0;
@@ -3369,73 +3201,8 @@ DEV uint64_t st_quad_bcast64(uint64_t x, uint32_t i) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-/* One sample of both channels on the fused path (T: position in the 8-sample group).  The
- * two channels' predictor sums, Rice decodes and cursor advances form one basic block (a
- * single wave-uniform branch to the rare cases), so their dependency chains interleave.
- * STG: the 16-bit stereo layouts, whose packed words stay in registers (pk: the group's two
- * 16-byte units) until the chunk's flush (st_flush_quad); other layouts store directly. */
-template <int T, int FMT>
-DEV void st_fused_step(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
-                       uint32_t nq, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al,
-                       uint32_t bs, bool store, u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1,
-                       uint32_t lane, bool anyw) {
-    constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
-    constexpr uint32_t spg = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u;
-    const uint32_t nqt = nq + ((!STG && T >= 4 && store) ? spg : 0u); /* + this group's direct store */
-    int32_t p0, p1, n0, n1;
-    st_fin2(z0, z1, z0.q[(T + 7) & 7], z1.q[(T + 7) & 7], pre0, pre1, p0, p1); /* this sample's prediction */
-    st_pre2<T>(z0, z1, n0, n1);                                                /* the next one's older taps */
-    pre0 = n0;
-    pre1 = n1;
-    const uint32_t w0 = br_peek(z0.b), w1 = br_peek(z1.b);
-    const uint32_t q0 = ffbh(w0), q1 = ffbh(w1); /* ~0u for an empty window: slow */
-    const bool sl0 = q0 >= z0.k32, sl1 = q1 >= z1.k32; /* prefix + stop bit + k bits overrun the window */
-    uint32_t u0 = (q0 << z0.k) | __builtin_amdgcn_ubfe(w0, z0.km - q0, z0.k);
-    uint32_t u1 = (q1 << z1.k) | __builtin_amdgcn_ubfe(w1, z1.km - q1, z1.k);
-    const uint32_t laneb = lane << 4;
-    st_adv_nc(z0.b, sl0 ? 0u : q0 + z0.k1, laneb);
-    st_adv_nc(z1.b, sl1 ? 0u : q1 + z1.k1, laneb);
-    /* landing check on even steps only: the words read now and at the next step must have
-     * landed (wi advances by at most one word per step) */
-    const bool ld0 = (T & 1) == 0 && z0.b.wi >= z0.b.vlim, ld1 = (T & 1) == 0 && z1.b.wi >= z1.b.vlim;
-    st_next_word(z0.b);
-    st_next_word(z1.b);
-    if (__builtin_expect(any_lane(sl0 || sl1 || ld0 || ld1), 0)) {
-        st_rare(z0, sl0, ld0, u0, limit, trunc, nqt, lane);
-        st_rare(z1, sl1, ld1, u1, limit, trunc, nqt, lane);
-    }
-    const int32_t s0 = (int32_t)(((u0 >> 1) ^ (0u - (u0 & 1u))) + (uint32_t)(p0 >> z0.sh));
-    const int32_t s1 = (int32_t)(((u1 >> 1) ^ (0u - (u1 & 1u))) + (uint32_t)(p1 >> z1.sh));
-    if (T & 1) {
-        st_range(z0, L[(T + 3) & 3], s0);
-        st_range(z1, R[(T + 3) & 3], s1);
-    }
-    z0.q[T] = __builtin_amdgcn_perm(z0.q[(T + 7) & 7], (uint32_t)s0, 0x05040100u);
-    z1.q[T] = __builtin_amdgcn_perm(z1.q[(T + 7) & 7], (uint32_t)s1, 0x05040100u);
-    L[T & 3] = s0;
-    R[T & 3] = s1;
-    if ((T & 3) == 3) {
-        if (__builtin_expect(anyw, 0)) { /* wasted bits (wave-uniform test) */
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                L[q] = (int32_t)((uint32_t)L[q] << z0.wasted);
-                R[q] = (int32_t)((uint32_t)R[q] << z1.wasted);
-            }
-        }
-        st_decor4(as_uni, as_u, as, L, R);
-        if (STG) {
-            uint32_t w[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_perm((uint32_t)R[q], (uint32_t)L[q], 0x05040100u);
-            pk[T >> 2] = u32x4{w[0], w[1], w[2], w[3]}; /* 16-byte unit 2g + (T >> 2) of the chunk's run */
-        } else if (store) {
-            st_emit4<FMT>(dst, nbase + (uint32_t)T - 3u, 4u, al, bs, L, R);
-        }
-    }
-}
-
-/* The restore and output half of st_fused_step for sample T of both channels, given the
- * folded Rice values u0 / u1 (zig-zag applied here). */
+/* The restore and output of sample T of both channels, given the folded Rice values u0 / u1
+ * (zig-zag applied here). */
 template <int T, int FMT, int AS = -1>
 DEV void st_lpc_out(StCh &z0, StCh &z1, uint32_t u0, uint32_t u1, int32_t (&L)[4], int32_t (&R)[4], bool as_uni,
                     uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al, uint32_t bs, bool store,
@@ -3520,7 +3287,7 @@ DEV void st_rare_pair(StCh &z, bool sl, bool ld, uint32_t &ua, uint32_t &ub, uin
     st_resync(z.b, lane);
 }
 /* Samples T and T + 1 (T even) of both channels: one window peek, one cursor advance and one
- * ring read per channel for two codewords (st_fused_step does one of each per codeword), then
+ * ring read per channel for two codewords, then
  * the two restores in order. */
 template <int T, int FMT, int AS = -1>
 DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
@@ -3641,11 +3408,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     const bool anyw = any_lane(ok && (z0.wasted | z1.wasted) != 0u);
     const uint32_t as_u = __builtin_amdgcn_readfirstlane(as);
     const bool as_uni = !any_lane(ok && as != as_u);
-    /* the fused chunks' compile-time assignment: one per wave, no wasted bits (BNF_ST_ASFIX=0: off) */
-#ifndef BNF_ST_ASFIX
-#define BNF_ST_ASFIX 1
-#endif
-    const int as_fix = (BNF_ST_ASFIX && as_uni && !anyw && as_u <= 3u) ? (int)as_u : -1;
+    /* the fused chunks' compile-time assignment: one per wave, no wasted bits */
+    const int as_fix = (as_uni && !anyw && as_u <= 3u) ? (int)as_u : -1;
     const uint32_t fl_unit = lane & 3u; /* the flush: this lane's 16-byte unit of a frame's 64-byte run */
     const bool podd = (lane & 1u) != 0, phi = (lane & 2u) != 0;
 
@@ -3685,15 +3449,9 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                         const uint32_t nq = nst + (STG ? 0u : g * 2u * ST_SPG); /* stores issued since the DMAs (at least) */
                         const uint32_t nb = n0 + g * 8u;
                         const bool sto = !(ablate & 2u);
-#if BNF_ST_PAIR
 #define FPAIR(T) st_fused_pair<T, FMT, AS>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
                         FPAIR(0); FPAIR(2); FPAIR(4); FPAIR(6);
 #undef FPAIR
-#else
-#define FSTEP(T) st_fused_step<T, FMT>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
-                        FSTEP(0); FSTEP(1); FSTEP(2); FSTEP(3); FSTEP(4); FSTEP(5); FSTEP(6); FSTEP(7);
-#undef FSTEP
-#endif
                         if (STG && g == 0) { pk01[0] = pk[0]; pk01[1] = pk[1]; }
                     }
                 };
@@ -3778,17 +3536,9 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         if (br_pos(z1.b) > limit) ok = false;
         resume = br_pos(z1.b);
     }
-    /* CRC-16: the k_parse launch's coalesced CRC pass covered [frame_off, next offset); a
-     * frame whose footer ends there and whose CRC was 0 is done.  Otherwise (the last frame
-     * of a batch, a gap before the next offset, a mismatch) the frame is re-read here. */
+    /* CRC-16 of the frame bytes (read_frame_'s footer check @0x10011a01) */
     uint32_t crc = crc_read;
-    const bool defer = (ablate & BNF_MODE_DEFER_CRC) != 0; /* k_crc_join checks it */
-    bool need = false;
-    if (ok && !defer) {
-        const uint32_t cn = info[f].crc_next;
-        const bool pre = (cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && fi.frame_off + (cn & BNF_CN_LEN) == end_byte + 2u;
-        need = !pre && !(ablate & 1u);
-    }
+    const bool need = ok && !(ablate & 1u);
     if (any_lane(need)) {
         wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
         lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
@@ -3800,9 +3550,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     if (ok) {
         info[f].resume_bit = resume;
         info[f].crc16_read = crc_read;
-        info[f].crc16_calc = defer ? 0u : crc;
-        info[f].crc_ok = defer ? 0u : 1u;
-        if (defer) info[f].flags = fi.flags | BNF_FL_CRC_DEFER;
+        info[f].crc16_calc = crc;
+        info[f].crc_ok = 1u;
     } else if (mine) {
         info[f].flags = fi.flags | BNF_FL_REDO;
     }
@@ -4197,12 +3946,9 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     const uint32_t as_u = __builtin_amdgcn_readfirstlane(as);
     const bool as_uni = !any_lane(ok && as != as_u);
     const bool all_wide = !any_lane(ok && !(z0.wide && z1.wide));
-#ifndef BNF_SW_FIX
-#define BNF_SW_FIX 1
-#endif
     /* the fused chunks' compile-time variant: the 64-bit path everywhere and one assignment,
      * M/S (C3) or independent; anything else runs the per-lane variant */
-    const int fix = (BNF_SW_FIX && as_uni && all_wide && as_u <= 3u) ? (int)as_u : -1;
+    const int fix = (as_uni && all_wide && as_u <= 3u) ? (int)as_u : -1;
 
     uint32_t mybs = ok ? bs : 0u;
     for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
@@ -4212,10 +3958,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     /* FILEREADER runs that start on a 64-byte line: the fused chunks flush whole lines
      * (sw_line_flush); the slots sit past the two rings (the CRC tables' extra 4 KB).
      * Ablation bit 0x20000000 (exact): per-lane 16-byte stores instead */
-#ifndef BNF_SW_LINE
-#define BNF_SW_LINE 1
-#endif
-    const bool line = BNF_SW_LINE && FMT == BNF_OUT_FILEREADER && sto && !hot && all_al && !(ablate & 0x20000000u) &&
+    const bool line = FMT == BNF_OUT_FILEREADER && sto && !hot && all_al && !(ablate & 0x20000000u) &&
                       !any_lane(ok && (((uintptr_t)dst) & 63u) != 0);
     lds_u32x4 *stg = (lds_u32x4 *)((lds_u32 *)ring + 2u * ST_RD * RING_LANE_DW);
     static_assert(sizeof(ring) >= (2u * ST_RD * RING_LANE_DW + 1024u) * 4u, "line slots past the rings");
@@ -4356,13 +4099,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
         resume = br_pos(z1.b);
     }
     uint32_t crc = crc_read;
-    const bool defer = (ablate & BNF_MODE_DEFER_CRC) != 0; /* k_crc_join checks it */
-    bool need = false;
-    if (ok && !defer) {
-        const uint32_t cn = info[f].crc_next;
-        const bool pre = (cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && fi.frame_off + (cn & BNF_CN_LEN) == end_byte + 2u;
-        need = !pre && !(ablate & 1u);
-    }
+    const bool need = ok && !(ablate & 1u);
     if (any_lane(need)) {
         wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
         lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
@@ -4374,9 +4111,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     if (ok) {
         info[f].resume_bit = resume;
         info[f].crc16_read = crc_read;
-        info[f].crc16_calc = defer ? 0u : crc;
-        info[f].crc_ok = defer ? 0u : 1u;
-        if (defer) info[f].flags = fi.flags | BNF_FL_CRC_DEFER;
+        info[f].crc16_calc = crc;
+        info[f].crc_ok = 1u;
     } else if (mine) {
         info[f].flags = fi.flags | BNF_FL_REDO;
     }
@@ -4658,7 +4394,6 @@ hipError_t bnf_stats(uint64_t *out16, int reset) {
 }
 
 /* words: 16-byte aligned; the allocation must cover round_up(nbytes, 16) bytes. */
-/* crc: also run the coalesced CRC pass over [offset f, offset f+1) (info.crc_next) */
 } /* extern "C" */
 
 /* Frame orders: counting sorts that put similar frames into the same wave (lane- and
@@ -4831,9 +4566,7 @@ static bool use_parse_wave(uint32_t nframes, const bnf_stream_params &sp) {
  * producer lane and a restore quad.  Auto: k_decode_sys while the lane kernels would have fewer
  * than SYS_AUTO_WAVES subframe waves (BNFLAC_SYS_WAVES overrides).
  * BNFLAC_DECODE_SYS=0 never, 1 always; bnf_set_decode_sys overrides. */
-#ifndef SYS_AUTO_WAVES
 #define SYS_AUTO_WAVES 1024u
-#endif
 static std::atomic<int> g_decode_sys{-1};
 static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32_t chn_lanes) {
     int m = g_decode_sys.load(std::memory_order_relaxed);
@@ -4864,23 +4597,11 @@ hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset) { /* debug counters o
     }
     return e;
 }
-/* crc: 0 none; 1 the CRC pass inside k_parse's launch; 2 k_crc on `side`, forked from s
- * (ev_fork) and finished at ev_crc, for bnf_launch_decode's deferred check */
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
                             bnf_stream_params sp, const uint64_t *out_sample_in, uint64_t base_sample,
-                            bnf_frame_info *info, int crc, uint32_t *order, hipStream_t side, hipEvent_t ev_fork,
-                            hipEvent_t ev_crc, hipStream_t s) {
+                            bnf_frame_info *info, uint32_t *order, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
-    if (crc == 2) {
-        hipError_t e = hipEventRecord(ev_fork, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(side, ev_fork, 0);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_crc, dim3((nframes + CRC_FPW - 1) / CRC_FPW), dim3(64), 0, side, words, nbytes, frame_offs,
-                           nframes, info);
-        e = hipEventRecord(ev_crc, side);
-        if (e != hipSuccess) return e;
-    }
-    if (crc == 0 && use_parse_wave(nframes, sp)) {
+    if (use_parse_wave(nframes, sp)) {
         static const uint32_t pws = getenv("BNFLAC_PW_STATS") ? 1u : 0u;
         static const int seg = [] { const char *e = getenv("BNFLAC_PW_SEG"); return e ? atoi(e) : 0; }();
         hipLaunchKernelGGL(k_parse_wave, dim3(nframes), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
@@ -4896,9 +4617,8 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
         hipError_t e = launch_order<1>(nullptr, (const uint8_t *)words, nbytes, frame_offs, nframes, order, &perm, s);
         if (e != hipSuccess) return e;
     }
-    const uint32_t np = (nframes + 63) / 64, nc = crc == 1 ? (nframes + CRC_FPW - 1) / CRC_FPW : 0u;
-    hipLaunchKernelGGL(k_parse, dim3(np + nc), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
-                       out_sample_in, base_sample, info, ablate_flags(), np, nc, perm, crc == 2 ? 1u : 0u);
+    hipLaunchKernelGGL(k_parse, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
+                       out_sample_in, base_sample, info, ablate_flags(), perm);
     return hipGetLastError();
 }
 
@@ -4913,12 +4633,12 @@ hipError_t bnf_launch_fill_bad(const bnf_frame_info *info, uint32_t nframes, bnf
 
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                              uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                             uint32_t *order, hipEvent_t ev_crc, hipStream_t s) {
+                             uint32_t *order, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
-    uint32_t mode = ev_crc ? BNF_MODE_DEFER_CRC : 0u; /* a concurrent CRC pass is running (k_crc) */
+    uint32_t mode = 0;
     /* every frame through k_decode_sys (decode order by class and blocksize), then its
      * hand-backs through k_decode_list; order scratch: 256 + nframes (perm) + 4 + nframes (list) */
-    if (order && !ev_crc && use_decode_sys(nframes, sp, chn_lanes)) {
+    if (order && use_decode_sys(nframes, sp, chn_lanes)) {
         const uint32_t *perm = nullptr;
         uint32_t *list = order + 256u + nframes;
         hipError_t e = hipMemsetAsync(list, 0, 16, s);
@@ -5002,14 +4722,6 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
     } else {
         if (e == hipSuccess) e = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, s);
         if (e == hipSuccess) e = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, s);
-    }
-    if (e == hipSuccess && ev_crc) {
-        e = hipStreamWaitEvent(s, ev_crc, 0);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_crc_join, dim3((nframes + 255) / 256), dim3(256), 0, s, (const uint8_t *)words, nframes,
-                               sp, fmt, out, info);
-            e = hipGetLastError();
-        }
     }
     return e;
 }

@@ -44,12 +44,11 @@ void bnf_set_ablate(uint32_t v);
 hipError_t bnf_stats(uint64_t *out16, int reset);
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs,
                             uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
-                            uint64_t base_sample, bnf_frame_info *info, int crc, uint32_t *order, hipStream_t side,
-                            hipEvent_t ev_fork, hipEvent_t ev_crc, hipStream_t s);
+                            uint64_t base_sample, bnf_frame_info *info, uint32_t *order, hipStream_t s);
 /* order: nullptr, or 256 + nframes words of device scratch for the frame order (k_order_*) */
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes,
                              bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
-                             bnf_frame_info *info, uint32_t *order, hipEvent_t ev_crc, hipStream_t s);
+                             bnf_frame_info *info, uint32_t *order, hipStream_t s);
 hipError_t bnf_launch_fill_bad(const bnf_frame_info *info, uint32_t nframes, bnf_stream_params sp, int fmt,
                                uint8_t *out, uint64_t out_bytes, hipStream_t s);
 hipError_t bnf_launch_chain(const uint8_t *bytes, uint64_t nbytes, const uint64_t *cand, uint32_t ncand,
@@ -136,21 +135,6 @@ static int ensure_device(int dev) {
  * bit4 k_parse subframe walk.  0x2000 is an exact A/B switch: the 24-bit FLACFileReader
  * wide flush (pack_wide24) off. */
 extern "C" BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags) { bnf_set_ablate(flags); }
-/* Coalesced CRC pass of the batch API (frame record crc_next; the decode kernels then skip
- * their own CRC re-read for frames it vouches for).  1: fused into the k_parse launch;
- * 2: k_crc on a second stream beside k_parse and the decode kernels, the verdict in
- * k_crc_join.  Off by default: the table-driven CRC of 11 GB costs about what the re-read
- * saves (C2, B = 1024: mode 1 parse +2.3 ms, decode -2.2 ms; mode 2 step 17.0 -> 19.0 ms),
- * see DESIGN.md section 9.  BNFLAC_CRC_PASS=1|2 turns it on; results are identical. */
-static int g_crc_pass = -1;
-static int crc_pass() { /* 0 off, 1 inside k_parse's launch, 2 concurrent (k_crc on a second stream) */
-    if (g_crc_pass < 0) {
-        const char *e = getenv("BNFLAC_CRC_PASS");
-        g_crc_pass = e ? std::min(std::max(atoi(e), 0), 2) : 0;
-    }
-    return g_crc_pass;
-}
-extern "C" BNFLAC_API void bnflac_debug_set_crc_pass(int on) { g_crc_pass = std::min(std::max(on, 0), 2); }
 extern "C" void bnf_set_parse_wave(int mode);
 /* parse kernel: -1 auto (k_parse_wave for small launches), 0 k_parse, 1 k_parse_wave (tests, A/B) */
 extern "C" BNFLAC_API void bnflac_debug_set_parse_wave(int mode) { bnf_set_parse_wave(mode); }
@@ -203,12 +187,6 @@ struct bnflac_ctx {
     /* bnflac_index_stream scratch */
     CtxBuf cand, info, gap, jump, mark, pos, bs, small;
     CtxBuf order, porder; /* decode / parse order: histogram + permutation (k_order_*) */
-    /* concurrent CRC pass (crc_pass() == 2): k_crc runs on `side`; the decode of the same
-     * record array (pending_info, pending_n) waits for ev_crc before k_crc_join */
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_crc = nullptr;
-    const void *pending_info = nullptr;
-    uint32_t pending_n = 0;
 };
 
 extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
@@ -223,10 +201,6 @@ extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
 extern "C" BNFLAC_API void bnflac_ctx_destroy(bnflac_ctx *ctx) {
     if (!ctx) return;
     if (ctx->d_block_counts) (void)hipFree(ctx->d_block_counts);
-    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
-    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-    if (ctx->ev_crc) (void)hipEventDestroy(ctx->ev_crc);
-    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     for (CtxBuf *b : {&ctx->cand, &ctx->info, &ctx->gap, &ctx->jump, &ctx->mark, &ctx->pos, &ctx->bs, &ctx->small,
                       &ctx->order, &ctx->porder})
         b->release();
@@ -298,20 +272,9 @@ extern "C" BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_
     memcpy(&p, sp, sizeof p);
     if (!ctx->porder.grow(sizeof(uint32_t) * (256u + (size_t)nframes)))
         return fail("bnflac_parse_frames: out of device memory (parse-order scratch)");
-    int crc = crc_pass();
-    if (crc == 2 && !ctx->side &&
-        (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
-         hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&ctx->ev_crc, hipEventDisableTiming) != hipSuccess))
-        return fail("bnflac_parse_frames: cannot create the CRC stream");
-    ctx->pending_info = nullptr;
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, d_frame_offsets,
-                                    nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info, crc,
-                                    (uint32_t *)ctx->porder.p, ctx->side, ctx->ev_fork, ctx->ev_crc, (hipStream_t)hs);
-    if (e == hipSuccess && crc == 2) {
-        ctx->pending_info = d_info;
-        ctx->pending_n = nframes;
-    }
+                                    nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info,
+                                    (uint32_t *)ctx->porder.p, (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_parse: ") + hipGetErrorString(e));
 }
 
@@ -326,22 +289,9 @@ extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d
     /* decode order (256 + nframes) + k_decode_sys's hand-back list (4 + nframes) */
     if (!ctx->order.grow(sizeof(uint32_t) * (260u + 2u * (size_t)nframes)))
         return fail("bnflac_decode_parsed: out of device memory (decode-order scratch)");
-    /* the records of this call came from bnflac_parse_frames with the concurrent CRC pass:
-     * the decode defers the check to k_crc_join after it */
-    const bool match = ctx->pending_info == d_info && ctx->pending_n == nframes;
-    hipEvent_t ev = match ? ctx->ev_crc : nullptr;
-    if (!match && ctx->pending_info) {
-        /* another record array (or a subset of the pending one) while k_crc may still be
-         * writing crc_next: the decode must not read a crc_next k_crc has not written yet
-         * (it would trust a stale VALID|ZERO word and skip the CRC-16 check), so it waits for
-         * the pass to finish and checks the frames itself */
-        if (hipStreamWaitEvent((hipStream_t)hs, ctx->ev_crc, 0) != hipSuccess)
-            return fail("bnflac_decode_parsed: cannot wait for the CRC pass");
-    }
-    ctx->pending_info = nullptr;
     hipError_t e = bnf_launch_decode((const uint32_t *)d_bytes, nbytes, nframes, p,
                                      lanes_for(sp->channels), out_format, d_out, out_bytes, (bnf_frame_info *)d_info,
-                                     (uint32_t *)ctx->order.p, ev, (hipStream_t)hs);
+                                     (uint32_t *)ctx->order.p, (hipStream_t)hs);
     if (e == hipSuccess) /* a non-OK frame's range: zeros (include/bnflac.h) */
         e = bnf_launch_fill_bad((const bnf_frame_info *)d_info, nframes, p, out_format, d_out, out_bytes, (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_decode: ") + hipGetErrorString(e));
@@ -391,7 +341,7 @@ extern "C" BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_
     memcpy(&p, sp, sizeof p);
     /* 2. header, CRC-8 and subframe walk of every candidate */
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, p, nullptr,
-                                    0, (bnf_frame_info *)ctx->info.p, 0, nullptr, nullptr, nullptr, nullptr, s);
+                                    0, (bnf_frame_info *)ctx->info.p, nullptr, s);
     /* 3. successor chain, EOS rule, compaction */
     if (e == hipSuccess)
         e = bnf_launch_chain(d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, (const bnf_frame_info *)ctx->info.p,
@@ -841,7 +791,7 @@ bool decode_window(Dec *d, uint64_t base) {
             }
             if (!d->d_info.grow(sizeof(bnf_frame_info) * ncand)) goto oom;
             if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, n, (const uint64_t *)d->d_cand.p, ncand, sp,
-                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, 0, nullptr, nullptr, nullptr, nullptr, d->stream) != hipSuccess)
+                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, nullptr, d->stream) != hipSuccess)
                 goto hip_fail;
             if (hipMemcpyAsync(d->info.data(), d->d_info.p, sizeof(bnf_frame_info) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
                 goto hip_fail;
@@ -863,7 +813,7 @@ bool decode_window(Dec *d, uint64_t base) {
             spd.channels = pcm_ch;
             if (bnf_launch_decode((const uint32_t *)d->d_bytes.p, n, ncand, spd, lanes_for(pcm_ch), BNF_OUT_PLANAR32,
                                   (uint8_t *)d->d_pcm.p, (uint64_t)std::max<uint64_t>(tot, 1) * pcm_ch * 4,
-                                  (bnf_frame_info *)d->d_info.p, nullptr, nullptr, d->stream) != hipSuccess)
+                                  (bnf_frame_info *)d->d_info.p, nullptr, d->stream) != hipSuccess)
                 goto hip_fail;
             d->pcm.resize((size_t)tot * pcm_ch);
             if (tot && hipMemcpyAsync(d->pcm.data(), d->d_pcm.p, sizeof(int32_t) * (size_t)tot * pcm_ch, hipMemcpyDeviceToHost, d->stream) != hipSuccess)

@@ -651,22 +651,21 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
             if (fmt == BNF_OUT_FLACDECODER && fi.bps != 16) unsupported = 1;          /* WriteCallback abort :526-530 */
             if (fmt >= BNF_OUT_FLACDECODER && fi.channels > sp.channels) unsupported = 1;
             if (fmt == BNF_OUT_FILEREADER && sp.bps != 16 && sp.bps != 24) unsupported = 1; /* NotSupportedException :239-240 */
-            if (unsupported) {
+            /* decode_block's outcome bits, each tested on its own (bit 2: the layout cannot
+             * carry the frame, bit 1: it ends past out_bytes; both may be set) */
+            uint64_t stride;
+            switch (fmt) {
+            case BNF_OUT_PLANAR32: case BNF_OUT_INTERLEAVED32: stride = 4ull * sp.channels; break;
+            case BNF_OUT_FLACDECODER: stride = fi.channels == 2 ? 4u : 2u; break;
+            default: stride = (uint64_t)sp.channels * (sp.bps == 24 ? 3u : 2u); break;
+            }
+            const bool past = (fi.out_sample + fi.blocksize) * stride > out_bytes;
+            if (unsupported || past) {
                 ok = false;
                 info[f].status = BNF_ST_SKIPPED;
-                info[f].flags = fi.flags | 4u;
+                info[f].flags = fi.flags | (unsupported ? 4u : 0u) | (past ? 2u : 0u);
             } else {
-                uint64_t stride;
-                switch (fmt) {
-                case BNF_OUT_PLANAR32: case BNF_OUT_INTERLEAVED32: stride = 4ull * sp.channels; break;
-                case BNF_OUT_FLACDECODER: stride = fi.channels == 2 ? 4u : 2u; break;
-                default: stride = (uint64_t)sp.channels * (sp.bps == 24 ? 3u : 2u); break;
-                }
-                if ((fi.out_sample + fi.blocksize) * stride > out_bytes) {
-                    ok = false;
-                    info[f].status = BNF_ST_SKIPPED;
-                    info[f].flags = fi.flags | 2u;
-                } else if (fi.channels > chn_lanes) {
+                if (fi.channels > chn_lanes) {
                     ok = false;
                     info[f].status = BNF_ST_SKIPPED;
                 }
@@ -923,13 +922,8 @@ __global__ void __launch_bounds__(SYS_THREADS) k_decode_sys(const uint32_t *__re
         }
         const uint64_t f_off = S.f_off[fl], end_byte = f_off + S.f_end[fl];
         const uint32_t crc_read = S.f_crc[fl];
-        bool pre = false;
-        {
-            const uint32_t cn = info[f].crc_next;
-            pre = (cn & BNF_CN_VALID) && (cn & BNF_CN_ZERO) && f_off + (cn & BNF_CN_LEN) == end_byte + 2u;
-        }
         uint32_t acc = 0;
-        if (!pre && !(ablate & 1u)) {
+        if (!(ablate & 1u)) {
             if (!have_lanec) {
                 lanec = crc16_shift(1u, 16u * (63u - lane));
                 have_lanec = true;

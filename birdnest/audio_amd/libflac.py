@@ -124,7 +124,7 @@ DECODER_SYMBOLS = [
 ]
 BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error", "bnflac_device_count",
                  "bnflac_index_frames", "bnflac_decode_frames", "bnflac_parse_frames", "bnflac_decode_parsed",
-                 "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats", "bnflac_debug_set_crc_pass", "bnflac_debug_set_parse_wave", "bnflac_debug_parse_wave_stats",
+                 "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats", "bnflac_debug_set_parse_wave", "bnflac_debug_parse_wave_stats",
                  "bnflac_debug_set_decode_sys", "bnflac_debug_decode_seg_launches", "bnflac_md5_interleaved32", "bnflac_index_stream"]
 READER_SYMBOLS = ["bnflac_reader_open", "bnflac_reader_params", "bnflac_reader_read", "bnflac_reader_close",
                   "bnflac_reader_last_error", "bnflac_reader_seek", "bnflac_reader_read_filereader",
@@ -174,7 +174,6 @@ def load() -> ctypes.CDLL:
     L.bnflac_decode_parsed.restype = i
     L.bnflac_decode_parsed.argtypes = [p, p, ctypes.c_uint64, ctypes.c_uint32, p, i, p, ctypes.c_uint64, p, p]
     L.bnflac_debug_set_ablate.argtypes = [ctypes.c_uint32]
-    L.bnflac_debug_set_crc_pass.argtypes = [ctypes.c_int]
     L.bnflac_debug_set_parse_wave.argtypes = [ctypes.c_int]
     L.bnflac_debug_set_decode_sys.argtypes = [ctypes.c_int]
     L.bnflac_debug_decode_seg_launches.restype, L.bnflac_debug_decode_seg_launches.argtypes = ctypes.c_uint64, []
@@ -297,7 +296,7 @@ FRAME_INFO_DTYPE = np.dtype([
     ("blocksize", "<u4"), ("sample_rate", "<u4"), ("channels", "<u4"), ("assignment", "<u4"), ("bps", "<u4"),
     ("number_type", "<u4"), ("unparseable", "<u4"), ("number", "<u8"), ("out_sample", "<u8"), ("crc8", "<u4"),
     ("crc16_calc", "<u4"), ("crc16_read", "<u4"), ("crc_ok", "<u4"), ("sub_start", "<u4", (8,)), ("flags", "<u4"),
-    ("crc_next", "<u4")])
+    ("reserved", "<u4")])
 assert FRAME_INFO_DTYPE.itemsize == FRAME_INFO_BYTES
 
 
@@ -386,11 +385,13 @@ class BatchDecoder:
         return d_offs, d_os, d_info, int(d_n.item())
 
     def decode_frames(self, d_bytes, nbytes: int, d_offsets, nframes: int, sp: StreamParams, fmt: int, d_out,
-                      d_info, d_out_sample=None, base_sample: int = 0, stream=None):
+                      d_info, d_out_sample=None, base_sample: int = 0, stream=None, out_bytes=None):
+        """out_bytes: the output size passed to the library (default: all of d_out)"""
+        nout = d_out.numel() * d_out.element_size()
         rc = self.L.bnflac_decode_frames(
             self.ctx, ctypes.c_void_p(d_bytes.data_ptr()), nbytes, ctypes.c_void_p(d_offsets.data_ptr()), nframes,
             ctypes.byref(sp), ctypes.c_void_p(d_out_sample.data_ptr()) if d_out_sample is not None else None,
-            base_sample, fmt, ctypes.c_void_p(d_out.data_ptr()), d_out.numel() * d_out.element_size(),
+            base_sample, fmt, ctypes.c_void_p(d_out.data_ptr()), nout if out_bytes is None else min(out_bytes, nout),
             ctypes.c_void_p(d_info.data_ptr()), self._stream(stream))
         if rc != 0:
             raise RuntimeError(self.L.bnflac_last_error().decode())

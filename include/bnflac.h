@@ -108,8 +108,7 @@ typedef struct {
     uint32_t sub_start[8];
     uint32_t flags;         /* bit 1: past out_bytes (status 3), bit 2: layout cannot carry it (status 3); the other
                                bits record the decode path (which kernel, hand-backs) and differ between paths */
-    uint32_t crc_next;      /* k_parse's CRC pass: bit31 valid, bit30 CRC-16 of [frame_off, next offset) is 0,
-                               bits 0-29 that length (0 when not computed) */
+    uint32_t reserved;      /* 0 */
 } bnflac_frame_info;
 
 enum {
@@ -182,12 +181,6 @@ BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uin
  * bit2 restore, bit3 Rice decode, bit4 subframe walk).  Output is wrong while set.
  * Exception: bit 0x800 only routes every k_decode chunk through the generic path (exact). */
 BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags);
-/* Mode switch (results stay exact): run the coalesced CRC-16 pass (frame record crc_next)
- * so the decode kernels skip their own CRC re-read for the frames it vouches for.
- * 1: inside bnflac_parse_frames' launch; 2: on a second stream, concurrent with the parse
- * and the decode of the same records (bnflac_decode_parsed then finishes the check).
- * Default 0 (env BNFLAC_CRC_PASS=1|2). */
-BNFLAC_API void bnflac_debug_set_crc_pass(int on);
 /* Development / test switch: parse kernel (-1 auto, 0 lane-per-frame k_parse, 1 wave-per-frame
  * k_parse_wave); both write identical records. */
 BNFLAC_API void bnflac_debug_set_parse_wave(int mode);

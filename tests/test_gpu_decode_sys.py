@@ -40,7 +40,8 @@ def _sp(libflac, data):
                                 ((x >> 41) & 7) + 1, ((x >> 36) & 31) + 1, x & ((1 << 36) - 1))
 
 
-def _decode(gpu, data, offs, fmt, sys_on, sp):
+def _decode(gpu, data, offs, fmt, sys_on, sp, out_frac=None):
+    """out_frac: pass only that fraction of the output buffer as out_bytes (frames past it SKIPPED)"""
     torch, libflac, dec, L = gpu
     dev = torch.device("cuda:0")
     d_bytes = torch.zeros((len(data) + 15) // 16 * 16 + 32, dtype=torch.uint8, device=dev)
@@ -52,7 +53,8 @@ def _decode(gpu, data, offs, fmt, sys_on, sp):
     d_info = torch.zeros(len(offs) * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
     L.bnflac_debug_set_decode_sys(1 if sys_on else 0)
     try:
-        dec.decode_frames(d_bytes, len(data), d_offs, len(offs), sp, fmt, d_out, d_info)
+        out_bytes = None if out_frac is None else int(total * stride * out_frac)
+        dec.decode_frames(d_bytes, len(data), d_offs, len(offs), sp, fmt, d_out, d_info, out_bytes=out_bytes)
         torch.cuda.synchronize()
     finally:
         L.bnflac_debug_set_decode_sys(-1)
@@ -70,17 +72,17 @@ def _frame_range(libflac, fmt, info, i, stride):
     if fmt == libflac.OUT_FLACDECODER:
         w = 4 if C == 2 else 2
         return os_ * w, bs * w
-    if fmt == libflac.OUT_PLANAR32:
-        return os_ * stride, bs * 4 * C
+    if fmt == libflac.OUT_PLANAR32:  # k_fill_bad stops at the batch's channel count (stride / 4)
+        return os_ * stride, bs * 4 * min(C, stride // 4)
     return os_ * stride, bs * stride
 
 
-def _same(gpu, data, offs, fmt):
+def _same(gpu, data, offs, fmt, out_frac=None):
     """lane kernels vs k_decode_sys: records, and the PCM of every frame that decodes"""
     torch, libflac, _, _ = gpu
     sp = _sp(libflac, data)
-    a, oa, stride = _decode(gpu, data, offs, fmt, False, sp)
-    b, ob, _ = _decode(gpu, data, offs, fmt, True, sp)
+    a, oa, stride = _decode(gpu, data, offs, fmt, False, sp, out_frac)
+    b, ob, _ = _decode(gpu, data, offs, fmt, True, sp, out_frac)
     for k in FIELDS:
         bad = np.nonzero(a[k] != b[k])[0]
         assert len(bad) == 0, f"{k} differs at frame {bad[0]} (offset {offs[bad[0]]}): lane {a[bad[0]]} sys {b[bad[0]]}"
@@ -98,6 +100,14 @@ def _same(gpu, data, offs, fmt):
     return n, b
 
 
+def _oracle_interleaved(data, out, nsamples, channels):
+    """the batch output of a valid stream in INTERLEAVED32 equals the oracle's decode"""
+    import oracle
+    ev, opcm = oracle.run(data)
+    pcm = out[:nsamples * 4 * channels].view("<i4").reshape(-1, channels)
+    assert np.array_equal(pcm, oracle.interleave(ev, opcm)), "differs from the oracle"
+
+
 def _offsets(s):
     return [int(x) for x in s.frame_offsets]
 
@@ -108,6 +118,10 @@ def test_fixtures_identical(gpu, name):
     data = open(os.path.join(GOLD_DIR, GOLD[name]["file"]), "rb").read()
     n, _ = _same(gpu, data, GOLD[name]["frame_offsets"], libflac.OUT_INTERLEAVED32)
     assert n == len(GOLD[name]["frame_offsets"])
+    sp = _sp(libflac, data)
+    if sp.has_stream_info and sp.total_samples:
+        _, out, _ = _decode(gpu, data, GOLD[name]["frame_offsets"], libflac.OUT_INTERLEAVED32, True, sp)
+        _oracle_interleaved(data, out, sp.total_samples, sp.channels)
 
 
 @pytest.mark.parametrize("fmt_name", ["OUT_PLANAR32", "OUT_INTERLEAVED32", "OUT_FLACDECODER", "OUT_FILEREADER"])
@@ -123,6 +137,10 @@ def test_configs_identical(gpu, fmt_name, cfg, kw):
     fmt = getattr(libflac, fmt_name)
     s = synth.encode(synth.config(cfg, **({"nframes": 12, "last_blocksize": 0} | kw)))
     _same(gpu, s.data.tobytes(), _offsets(s), fmt)
+    if fmt == libflac.OUT_INTERLEAVED32:  # anchored on the oracle, not only on the lane kernels
+        data = s.data.tobytes()
+        _, out, _ = _decode(gpu, data, _offsets(s), fmt, True, _sp(libflac, data))
+        _oracle_interleaved(data, out, s.nsamples, s.pcm.shape[1])
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
@@ -176,11 +194,14 @@ def test_fixed_24bit_side_leaves_24_bits(gpu, order, stereo):
     assert np.array_equal(out[:s.nsamples * 8].view("<i4").reshape(-1, 2), s.pcm)
 
 
-def test_damaged_and_truncated_identical(gpu):
+@pytest.mark.parametrize("fmt_name", ["OUT_INTERLEAVED32", "OUT_PLANAR32", "OUT_FLACDECODER", "OUT_FILEREADER"])
+def test_damaged_and_truncated_identical(gpu, fmt_name):
     """Byte flips (CRC failures, damaged residuals and headers) and cut streams: same records,
-    same PCM for every frame that decodes, CRC-failed frames zero-filled."""
+    same PCM for every frame that decodes, CRC-failed frames zero-filled, ERROR / TRUNC frames
+    zero-filled within their own slot (k_fill_bad) in every layout."""
     from birdnest.audio_amd import synth
     torch, libflac, _, _ = gpu
+    fmt = getattr(libflac, fmt_name)
     rng = np.random.default_rng(91)
     for i in range(16):
         cfg = ["C1", "C2", "C3", "C4", "C5"][i % 5]
@@ -193,7 +214,21 @@ def test_damaged_and_truncated_identical(gpu):
         if i % 3 == 2:
             data = data[:len(data) * 3 // 4]
             offs = [o for o in offs if o < len(data)]
-        _same(gpu, bytes(data), offs, libflac.OUT_INTERLEAVED32)
+        _same(gpu, bytes(data), offs, fmt)
+
+
+@pytest.mark.parametrize("cfg", ["C3", "C5"])
+def test_unsupported_and_short_buffer_flags(gpu, cfg):
+    """24-bit frames into the 16-bit FLACDecoder layout (unsupported, flag bit 2) with an output
+    buffer cut to 60% (the later frames also end past out_bytes, bit 1): both outcome bits are
+    set independently, the same on k_decode_sys and the lane kernels (decode_block)."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _, _ = gpu
+    s = synth.encode(synth.config(cfg, nframes=10, last_blocksize=0))
+    n, b = _same(gpu, s.data.tobytes(), _offsets(s), libflac.OUT_FLACDECODER, out_frac=0.6)
+    assert n == 0 and (b["status"] == 3).all()
+    fl = b["flags"] & 6
+    assert (fl & 4).all() and (fl == 6).any() and (fl == 4).any()
 
 
 def test_crc_mismatch_zero_filled(gpu):

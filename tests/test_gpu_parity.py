@@ -232,48 +232,12 @@ def test_crc_mismatch_zero_filled_in_batch(gpu):
                           np.delete(s.pcm, np.s_[2 * 4096: 3 * 4096], axis=0))
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-def test_crc_pass_records_and_fallbacks(gpu, mode):
-    """The coalesced CRC pass (frame record crc_next), inside the k_parse launch (mode 1) or
-    as k_crc on a second stream with the verdict in k_crc_join (mode 2): valid and zero for
-    intact frames followed by another offset, not zero for a corrupted frame, absent for the
-    last frame; frames whose footer does not end at the next offset (junk in between) and the
-    last frame still get their CRC-16 checked (decode kernels / k_crc_join)."""
+def test_crc_mismatch_and_junk_gap(gpu):
+    """A CRC-corrupted frame, junk bytes between two frames (the footer no longer ends at the
+    next offset) and the last frame of the batch: every CRC-16 is checked by the decode
+    kernels, the corrupted frame alone fails it and is zero-filled."""
     from birdnest.audio_amd import synth
     torch, libflac, _ = gpu
-    libflac.load().bnflac_debug_set_crc_pass(mode)
-    try:
-        _crc_pass_cases(gpu, synth, libflac)
-    finally:
-        libflac.load().bnflac_debug_set_crc_pass(0)
-
-
-@pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C5"])
-def test_crc_pass_modes_identical(gpu, cfg):
-    """Every CRC mode gives the same PCM and the same frame records (crc_next aside), with
-    no deferred-check flag left behind."""
-    from birdnest.audio_amd import synth
-    torch, libflac, _ = gpu
-    s = synth.encode(synth.config(cfg, nframes={"C4": 96}.get(cfg, 24), last_blocksize=0))
-    res = []
-    for mode in (0, 1, 2):
-        libflac.load().bnflac_debug_set_crc_pass(mode)
-        try:
-            res.append(_decode_batch(gpu, s.data.tobytes(), s.frame_offsets, libflac.OUT_INTERLEAVED32))
-        finally:
-            libflac.load().bnflac_debug_set_crc_pass(0)
-    for out, info, _ in res[1:]:
-        assert out.tobytes() == res[0][0].tobytes()
-        for n in info.dtype.names:
-            if n == "flags":  # bits 1-2 are outcomes; the rest is decode-path bookkeeping (include/bnflac.h)
-                assert np.array_equal(info[n] & 6, res[0][1][n] & 6), n
-            elif n != "crc_next":
-                assert np.array_equal(info[n], res[0][1][n]), n
-    assert not (res[2][1]["flags"] & 256).any()
-    assert (res[0][1]["crc_ok"] == 1).all()
-
-
-def _crc_pass_cases(gpu, synth, libflac):
     for cfg in ("C2", "C3", "C4"):
         s = synth.encode(synth.config(cfg, nframes=8, last_blocksize=0))
         d = bytearray(s.data.tobytes())
@@ -283,11 +247,6 @@ def _crc_pass_cases(gpu, synth, libflac):
         d = d[: o[6]] + junk + d[o[6]:]
         o = o[:6] + [x + len(junk) for x in o[6:]]
         out, info, sp = _decode_batch(gpu, bytes(d), o, libflac.OUT_INTERLEAVED32)
-        cn = info["crc_next"].astype(np.int64)
-        valid, zero, ln = (cn >> 31) & 1, (cn >> 30) & 1, cn & 0x3FFFFFFF
-        assert valid[:7].all() and valid[7] == 0, cfg
-        assert list(ln[:7]) == [o[i + 1] - o[i] for i in range(7)], cfg
-        assert zero[2] == 0 and zero[5] == 0 and zero[[0, 1, 3, 4, 6]].all(), cfg
         assert info["crc_ok"].tolist() == [1, 1, 0, 1, 1, 1, 1, 1], cfg
         assert (info["status"] == 0).all(), cfg
         pcm = out.view("<i4").reshape(-1, s.pcm.shape[1])
