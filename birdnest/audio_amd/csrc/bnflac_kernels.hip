@@ -45,11 +45,15 @@
 __constant__ uint8_t g_crc8_tab[256];
 __constant__ uint16_t g_crc16_tab[8][256]; /* slice-by-8 */
 __constant__ uint16_t g_crc16_xpow[40];    /* x^(8*2^j) mod P for j < 40 */
-/* CRC-16 of an 8-byte block by six fields of 11/11/10 bits (crc16_step8w): the contribution
- * of each field value to the block's CRC (init 0), fields at bit 53, 42, 32, 21, 10, 0 of the
- * big-endian block; the last field's first 256 entries are the byte table.  20 KB. */
+/* CRC-16 of an 8-byte block by six fields of 11/11/10 bits (crc16_step8le): the contribution
+ * of each field value to the block's CRC (init 0).  The fields are bits [0,11), [11,22) and
+ * [22,32) of the block's two words AS LOADED (little-endian: stream byte 0 in bits 0-7), so the
+ * step needs no byte swap, and every entry is stored byte-swapped, so the running CRC stays in
+ * that form and XORs straight into the first word's low 16 bits (round 5: the step is 18
+ * add / shift-right / and / xor, all full-rate, instead of 21 with two v_perm and four v_bfe).
+ * Table f at CRC11_OFF[f] entries: w0 fields 0-2, w1 fields 0-2.  20 KB. */
 #define CRC11_N 10240
-#define CRC11_BYTE 9216 /* offset of the last (10-bit) field's table = the byte table */
+#define CRC11_W1F2 9216 /* w1 bits [22,32): stream byte 7 = index bits 2-9, i.e. the byte table at x << 2 */
 __constant__ uint16_t g_crc16_t11[CRC11_N];
 
 /* Debug event counters (wave-level events, enabled by ablate bit 0x100; timing runs
@@ -1142,10 +1146,85 @@ DEV void wave_read_raw(WR &r, uint32_t cnt, uint32_t nb, int32_t *dst) {
     }
     r.pos = base + (uint64_t)cnt * nb;
 }
+/* Small partitions (round 5): a wave pass costs about the same whatever the partition size
+ * (window loads, the speculative walk, ~4 splice rounds), so a subframe of 256 partitions of
+ * 16 codewords paid 256 passes -- one C5 file whose encoder picked high partition orders took
+ * 0.85 ms to parse against 0.32 ms for the others, and set the 8-file launch at 0.96 ms
+ * (tools/c5_parse_ab.py).  Below PW_SCALAR_MAX samples per partition the whole residual is
+ * walked by the scalar unit instead: 64 stream words sit one per lane in a VGPR, the cursor is
+ * an SGPR, each codeword is two v_readlane, a 64-bit scalar shift, s_flbit and an add, and the
+ * partition headers are read the same way.  Same positions, TRUNC and slow-prefix rules as the
+ * pass (a window of 32 zero bits goes to br_unary). */
+#define PW_SCALAR_MAX 64u
+struct SWin { /* 64 stream words [base, base + 64) held one per lane */
+    uint32_t base, v;
+};
+DEV void swin_load(WR &r, SWin &s, uint32_t wi) {
+    s.base = wr_u(wi);
+    wr_need(r, s.base, s.base + 64u);
+    s.v = wr_word(r, s.base + (threadIdx.x & 63u));
+}
+/* the 32 bits at bit position pos (the window reloaded when pos leaves it) */
+DEV uint32_t swin_peek(WR &r, SWin &s, uint64_t pos) {
+    uint32_t wi = wr_u((uint32_t)(pos >> 5));
+    if (wi < s.base || wi + 1u >= s.base + 64u) swin_load(r, s, wi);
+    const uint32_t i = wi - s.base, sh = (uint32_t)pos & 31u;
+    const uint32_t hi = __builtin_amdgcn_readlane(s.v, i), lo = __builtin_amdgcn_readlane(s.v, i + 1u);
+    /* the shift-0 case apart: the 64-bit form compiled to a funnel shift that returned the
+     * low word at a word-aligned cursor */
+    return sh ? __builtin_amdgcn_alignbit(hi, lo, 32u - sh) : hi;
+}
+DEV uint32_t wave_skip_residual_scalar(WR &r, const SubHdr &h, uint32_t bs, uint64_t limit) {
+    const uint32_t parts = 1u << h.porder;
+    const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
+    const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
+    SWin s;
+    swin_load(r, s, wr_u((uint32_t)(r.pos >> 5)));
+    uint64_t pos = r.pos;
+    for (uint32_t p = 0; p < parts; p++) {
+        if (pos > limit) break; /* the previous partition ended past the buffer */
+        const uint32_t kk = swin_peek(r, s, pos) >> (32u - plen);
+        pos += plen;
+        uint32_t cnt = (h.porder == 0 || p > 0) ? psamples : psamples - h.order;
+        if (kk >= pesc) {
+            const uint32_t nb = swin_peek(r, s, pos) >> 27;
+            pos += 5u + (uint64_t)nb * cnt;
+            continue;
+        }
+        const uint32_t k1 = kk + 1u;
+        while (cnt) {
+            if (pos > limit) break;
+            const uint32_t w = swin_peek(r, s, pos);
+            if (w == 0u) { /* a unary prefix longer than the window: the generic reader */
+                r.pos = pos;
+                uint32_t q;
+                if (!br_unary(r, q, limit)) return BNF_ST_TRUNC;
+                pos = r.pos + kk;
+                cnt--;
+                swin_load(r, s, wr_u((uint32_t)(pos >> 5)));
+                continue;
+            }
+            const uint32_t la = (uint32_t)__builtin_clz(w) + k1;
+            /* a second codeword in the same window when both fit */
+            const uint32_t w2 = la < 32u ? (w << la) : 0u;
+            const uint32_t lb = w2 ? (uint32_t)__builtin_clz(w2) + k1 : 64u;
+            if (cnt >= 2u && la + lb <= 32u) {
+                pos += la + lb;
+                cnt -= 2u;
+            } else {
+                pos += la;
+                cnt--;
+            }
+        }
+    }
+    r.pos = pos;
+    return pos > limit ? BNF_ST_TRUNC : BNF_ST_OK;
+}
 DEV uint32_t wave_skip_residual(WR &r, const SubHdr &h, uint32_t bs, uint64_t limit, bool stats, int seg) {
     const uint32_t parts = 1u << h.porder;
     const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
     const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
+    if (psamples <= PW_SCALAR_MAX && seg >= 0) return wave_skip_residual_scalar(r, h, bs, limit);
     for (uint32_t p = 0; p < parts; p++) {
         if (br_pos(r) > limit) return BNF_ST_TRUNC; /* the previous partition ended past the buffer */
         const uint32_t kk = wr_u(br_read(r, plen));
@@ -1534,12 +1613,20 @@ DEV uint32_t crc16_step8(uint32_t crc, uint32_t w0, uint32_t w1, const lds_u16 *
            T[4 * 256 + (a & 0xff)] ^ T[3 * 256 + (w1 >> 24)] ^ T[2 * 256 + ((w1 >> 16) & 0xff)] ^
            T[1 * 256 + ((w1 >> 8) & 0xff)] ^ T[w1 & 0xff];
 }
-/* the same 8-byte step with 6 lookups instead of 8 (tables: g_crc16_t11 in LDS) */
-DEV uint32_t crc16_step8w(uint32_t crc, uint32_t w0, uint32_t w1, const lds_u16 *T) {
-    const uint32_t a = w0 ^ (crc << 16);
-    return T[a >> 21] ^ T[2048 + ((a >> 10) & 0x7ffu)] ^ T[4096 + (a & 0x3ffu)] ^ T[5120 + (w1 >> 21)] ^
-           T[7168 + ((w1 >> 10) & 0x7ffu)] ^ T[CRC11_BYTE + (w1 & 0x3ffu)];
+/* the same 8-byte step with 6 lookups instead of 8 (tables: g_crc16_t11 in LDS).  cs: the CRC
+ * so far, byte-swapped (its high byte in bits 0-7); w0, w1: the block's two words as loaded.
+ * The table offsets are byte offsets of field * 2, so each lookup address is one shift-right
+ * (or add) and one and. */
+DEV uint32_t crc16_t11_at(const lds_u16 *T, uint32_t boff) {
+    return *(const lds_u16 *)((const __attribute__((address_space(3))) uint8_t *)T + boff);
 }
+DEV uint32_t crc16_step8le(uint32_t cs, uint32_t w0, uint32_t w1, const lds_u16 *T) {
+    const uint32_t a = w0 ^ cs;
+    return crc16_t11_at(T, (a + a) & 0xFFEu) ^ crc16_t11_at(T, 4096u + ((a >> 10) & 0xFFEu)) ^
+           crc16_t11_at(T, 8192u + ((a >> 21) & 0x7FEu)) ^ crc16_t11_at(T, 10240u + ((w1 + w1) & 0xFFEu)) ^
+           crc16_t11_at(T, 14336u + ((w1 >> 10) & 0xFFEu)) ^ crc16_t11_at(T, 2u * CRC11_W1F2 + ((w1 >> 21) & 0x7FEu));
+}
+DEV uint32_t crc16_unswap(uint32_t cs) { return ((cs >> 8) | (cs << 8)) & 0xffffu; }
 DEV uint32_t crc16_range(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
     uint32_t crc = 0;
     uint64_t p = b0;
@@ -3063,8 +3150,7 @@ DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line o
 }
 #define CRC_LINES 4
 DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
-    const lds_u16 *Tb = T + CRC11_BYTE;
-    uint32_t crc = 0;
+    uint32_t crc = 0; /* byte-swapped until the trailing bytes (crc16_step8le) */
     /* whole lines from the one holding b0, its bytes below b0 taken as zeros (a CRC with
      * init 0 stays 0 over leading zero bytes) */
     const uint64_t p0 = b0 & ~(uint64_t)63u;
@@ -3093,8 +3179,8 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
                 if (i + d < nl) {
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        crc = crc16_step8w(crc, __builtin_bswap32(buf[d][u].x), __builtin_bswap32(buf[d][u].y), T);
-                        crc = crc16_step8w(crc, __builtin_bswap32(buf[d][u].z), __builtin_bswap32(buf[d][u].w), T);
+                        crc = crc16_step8le(crc, buf[d][u].x, buf[d][u].y, T);
+                        crc = crc16_step8le(crc, buf[d][u].z, buf[d][u].w, T);
                     }
                     const uint32_t j = min(i + d + CRC_LINES, nl - 1u);
 #pragma unroll
@@ -3111,10 +3197,12 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
         for (uint32_t i = 0; i < 7; i++) t8[i] = i < n8 ? q8[i] : make_uint2(0u, 0u);
 #pragma unroll
         for (uint32_t i = 0; i < 7; i++)
-            if (i < n8) crc = crc16_step8w(crc, __builtin_bswap32(t8[i].x), __builtin_bswap32(t8[i].y), T);
+            if (i < n8) crc = crc16_step8le(crc, t8[i].x, t8[i].y, T);
         p += 8u * n8;
     }
-    while (p < b1) { crc = ((crc << 8) ^ Tb[((crc >> 8) ^ bytes[p]) & 0xff]) & 0xffff; p++; }
+    crc = crc16_unswap(crc);
+    /* trailing bytes: the byte table is w1's [22,32) field table at byte << 2 (stream byte 7) */
+    while (p < b1) { crc = ((crc << 8) ^ crc16_unswap(T[CRC11_W1F2 + ((((crc >> 8) ^ bytes[p]) & 0xffu) << 2)])) & 0xffff; p++; }
     return crc;
 }
 
@@ -4140,16 +4228,23 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
     if (e != hipSuccess) return e;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_tab), crc16x8, 8 * 256 * sizeof(uint16_t));
     if (e != hipSuccess) return e;
-    { /* field tables from the byte table (crc16x8[0]): CRC of the 8-byte block v << shift */
-        static const uint32_t sh[6] = {53, 42, 32, 21, 10, 0}, wd[6] = {11, 11, 10, 11, 11, 10};
+    { /* field tables (crc16_step8le) from the byte table (crc16x8[0]): the CRC of the 8-byte
+       * block holding v in bits [lo, lo + wd) of word j as loaded (LE bit p of word j = stream
+       * byte 4j + p / 8, bit p % 8 of that byte), stored byte-swapped */
+        static const uint32_t lo[6] = {0, 11, 22, 0, 11, 22}, wd[6] = {11, 11, 10, 11, 11, 10}, wj[6] = {0, 0, 0, 1, 1, 1};
         uint16_t t11[CRC11_N];
         uint32_t at = 0;
         for (int fld = 0; fld < 6; fld++)
             for (uint32_t v = 0; v < (1u << wd[fld]); v++) {
-                const uint64_t m = (uint64_t)v << sh[fld];
+                uint8_t blk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                for (uint32_t i = 0; i < wd[fld]; i++)
+                    if ((v >> i) & 1u) {
+                        const uint32_t p = lo[fld] + i;
+                        blk[4u * wj[fld] + p / 8u] |= (uint8_t)(1u << (p % 8u));
+                    }
                 uint32_t c = 0;
-                for (int by = 7; by >= 0; by--) c = ((c << 8) ^ crc16x8[((c >> 8) ^ (uint32_t)(m >> (8 * by))) & 0xffu]) & 0xffffu;
-                t11[at++] = (uint16_t)c;
+                for (int by = 0; by < 8; by++) c = ((c << 8) ^ crc16x8[((c >> 8) ^ blk[by]) & 0xffu]) & 0xffffu;
+                t11[at++] = (uint16_t)(((c >> 8) | (c << 8)) & 0xffffu);
             }
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_t11), t11, sizeof t11);
         if (e != hipSuccess) return e;
