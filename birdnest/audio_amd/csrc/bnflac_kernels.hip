@@ -91,6 +91,14 @@ DEV u32x4 lds_ld128(const void *a) { /* result valid after s_waitcnt lgkmcnt(0) 
     asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)a) : "memory");
     return v;
 }
+DEV void lds_st128(const lds_u32x4 *a, u32x4 v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"((uint32_t)(uintptr_t)a), "v"(v) : "memory");
+}
+DEV u32x4 lds_ld128(const lds_u32x4 *a) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)a) : "memory");
+    return v;
+}
 DEV void lds_st64(const void *a, uint64_t v) {
     asm volatile("ds_write_b64 %0, %1" ::"v"((uint32_t)(uintptr_t)a), "v"(v) : "memory");
 }
@@ -2847,7 +2855,8 @@ __global__ void __launch_bounds__(256) k_chain_emit(const uint64_t *__restrict__
  * Frames it declines (VERBATIM/CONSTANT/64-bit-path subframes, errors, truncation, CRC
  * mismatch, out-of-range samples, unsupported layouts) get BNF_FL_REDO and are decoded
  * again, exactly, by k_decode<8>, which runs after it on the same stream. */
-#define ST_CHK 16 /* samples per chunk (one 64-byte FLACDecoder run per frame) */
+#define ST_CHK 16 /* samples per chunk of k_decode_sw (one 64-byte FLACDecoder run per frame) */
+#define ST2_CHK 32 /* samples per chunk of k_decode_st: one 128-byte FLACDecoder line per frame (round 5) */
 #define ST_RD 8  /* 16-byte ring slots per lane and channel: two 64-byte groups */
 
 struct StCh {
@@ -3291,10 +3300,10 @@ DEV uint64_t st_quad_bcast64(uint64_t x, uint32_t i) {
 
 /* The restore and output of sample T of both channels, given the folded Rice values u0 / u1
  * (zig-zag applied here). */
-template <int T, int FMT, int AS = -1>
+template <int T, int FMT, int AS, int PO, int NPK> /* PO: the group's first unit in pk */
 DEV void st_lpc_out(StCh &z0, StCh &z1, uint32_t u0, uint32_t u1, int32_t (&L)[4], int32_t (&R)[4], bool as_uni,
                     uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al, uint32_t bs, bool store,
-                    u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1, bool anyw) {
+                    u32x4 (&pk)[NPK], int32_t &pre0, int32_t &pre1, bool anyw) {
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     int32_t p0, p1, n0, n1;
     st_fin2(z0, z1, z0.q[(T + 7) & 7], z1.q[(T + 7) & 7], pre0, pre1, p0, p1); /* this sample's prediction */
@@ -3324,7 +3333,7 @@ DEV void st_lpc_out(StCh &z0, StCh &z1, uint32_t u0, uint32_t u1, int32_t (&L)[4
             uint32_t w[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_perm((uint32_t)R[q], (uint32_t)L[q], 0x05040100u);
-            pk[T >> 2] = u32x4{w[0], w[1], w[2], w[3]};
+            pk[PO + (T >> 2)] = u32x4{w[0], w[1], w[2], w[3]};
         } else if (store) {
             st_emit4<FMT>(dst, nbase + (uint32_t)T - 3u, 4u, al, bs, L, R);
         }
@@ -3377,10 +3386,10 @@ DEV void st_rare_pair(StCh &z, bool sl, bool ld, uint32_t &ua, uint32_t &ub, uin
 /* Samples T and T + 1 (T even) of both channels: one window peek, one cursor advance and one
  * ring read per channel for two codewords, then
  * the two restores in order. */
-template <int T, int FMT, int AS = -1>
+template <int T, int FMT, int AS, int PO, int NPK>
 DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uint64_t limit, uint32_t &trunc,
                        uint32_t nq, bool as_uni, uint32_t as_u, uint32_t as, uint8_t *dst, uint32_t nbase, bool al,
-                       uint32_t bs, bool store, u32x4 (&pk)[2], int32_t &pre0, int32_t &pre1,
+                       uint32_t bs, bool store, u32x4 (&pk)[NPK], int32_t &pre0, int32_t &pre1,
                        uint32_t lane, bool anyw) {
     static_assert((T & 1) == 0, "pairs start on even samples");
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
@@ -3403,8 +3412,8 @@ DEV void st_fused_pair(StCh &z0, StCh &z1, int32_t (&L)[4], int32_t (&R)[4], uin
         st_rare_pair(z0, sl0, ld0, u0a, u0b, limit, trunc, nqt, lane);
         st_rare_pair(z1, sl1, ld1, u1a, u1b, limit, trunc, nqt, lane);
     }
-    st_lpc_out<T, FMT, AS>(z0, z1, u0a, u1a, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
-    st_lpc_out<T + 1, FMT, AS>(z0, z1, u0b, u1b, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
+    st_lpc_out<T, FMT, AS, PO, NPK>(z0, z1, u0a, u1a, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
+    st_lpc_out<T + 1, FMT, AS, PO, NPK>(z0, z1, u0b, u1b, L, R, as_uni, as_u, as, dst, nbase, al, bs, store, pk, pre0, pre1, anyw);
 }
 
 /* One sample of both channels on the general path: warm-up, partition headers anywhere,
@@ -3498,28 +3507,40 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     const bool as_uni = !any_lane(ok && as != as_u);
     /* the fused chunks' compile-time assignment: one per wave, no wasted bits */
     const int as_fix = (as_uni && !anyw && as_u <= 3u) ? (int)as_u : -1;
-    const uint32_t fl_unit = lane & 3u; /* the flush: this lane's 16-byte unit of a frame's 64-byte run */
-    const bool podd = (lane & 1u) != 0, phi = (lane & 2u) != 0;
+    /* the flush's staging: the 4 KB past the two rings (the CRC tables' share of the LDS), not
+     * an LDS-DMA target */
+    lds_u32x4 *stg = (lds_u32x4 *)((lds_u32 *)ring + 2u * ST_RD * RING_LANE_DW);
 
     uint32_t mybs = ok ? bs : 0u;
     for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
-    const uint32_t nchunks = (mybs + ST_CHK - 1) / ST_CHK;
+    const uint32_t nchunks = (mybs + ST2_CHK - 1) / ST2_CHK;
     uint32_t trunc = 0;
     wait_vm(); /* setup loads done: the store count starts from zero */
     uint32_t nst = 0; /* vector-memory ops (PCM stores) issued by this wave since the last refill's DMAs */
+    const bool sto = !(ablate & 2u);
+    /* refill: wait for the previous refill's DMAs (every store since stays in flight), then
+     * issue the next blocks; stores issued after it are younger */
+    auto refill = [&](bool want) {
+        wait_vm_n(nst);
+        z0.b.vendw = z0.b.iend * 4u;
+        z1.b.vendw = z1.b.iend * 4u;
+        st_refill_issue(z0.b, want);
+        st_refill_issue(z1.b, want);
+        nst = 0;
+    };
     const uint64_t t_loop = tnow(tmon);
     for (uint32_t kc = 0; kc < nchunks; kc++) {
         const uint64_t ta = tnow(tmon);
-        const uint32_t n0 = kc * ST_CHK;
+        const uint32_t n0 = kc * ST2_CHK;
         const bool valid = ok && n0 < bs;
-        bool fast = valid && n0 >= 8u && n0 + ST_CHK <= bs && !(ablate & 12u);
+        bool fast = valid && n0 >= 8u && n0 + ST2_CHK <= bs && !(ablate & 12u);
         if (fast) { /* partition headers at the chunk boundary (aligned partitions) */
             if (z0.left == 0 && z0.pidx < z0.nparts) st_partition(z0);
             if (z1.left == 0 && z1.pidx < z1.nparts) st_partition(z1);
-            fast = !z0.esc && !z1.esc && z0.left >= ST_CHK && z1.left >= ST_CHK;
+            fast = !z0.esc && !z1.esc && z0.left >= ST2_CHK && z1.left >= ST2_CHK;
         }
         const bool fused = !any_lane(valid && !fast);
-        u32x4 pk[2], pk01[2]; /* the chunk's four 16-byte units (STG): pk01 from g = 0, pk from g = 1 */
+        u32x4 pk[4], pk0[4]; /* STG: the chunk's eight 16-byte units of this lane's frame run (128 bytes): pk0 from the first half, pk from the second */
         if (fused) {
             if (valid) {
                 STAT(z0.b.stats, 0);
@@ -3527,20 +3548,34 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                 st_pre2<7>(z0, z1, pre0, pre1); /* older taps of the chunk's first sample */
                 st_resync(z0.b, lane);
                 st_resync(z1.b, lane);
-                /* the chunk's 4 groups of 8 samples; AS >= 0: the wave's one assignment, no
-                 * wasted bits (st_decor4t), compiled per assignment */
+                /* the chunk's 4 groups of 8 samples, a refill after the second; AS >= 0: the
+                 * wave's one assignment, no wasted bits (st_decor4t), compiled per assignment */
                 auto chunk = [&](auto as_c) {
                     constexpr int AS = decltype(as_c)::value;
-#pragma unroll 1
-                    for (uint32_t g = 0; g < ST_CHK / 8; g++) {
+                    auto group = [&](auto g_c, uint32_t nb) {
+                        constexpr uint32_t G = decltype(g_c)::value;
                         int32_t L[4], R[4];
-                        const uint32_t nq = nst + (STG ? 0u : g * 2u * ST_SPG); /* stores issued since the DMAs (at least) */
-                        const uint32_t nb = n0 + g * 8u;
-                        const bool sto = !(ablate & 2u);
-#define FPAIR(T) st_fused_pair<T, FMT, AS>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
+                        const uint32_t nq = nst + (STG ? 0u : G * 2u * ST_SPG); /* stores issued since the DMAs (at least) */
+#define FPAIR(T) st_fused_pair<T, FMT, AS, 2 * G, 4>(z0, z1, L, R, limit, trunc, nq, as_uni, as_u, as, dst, nb, al, bs, sto, pk, pre0, pre1, lane, anyw)
                         FPAIR(0); FPAIR(2); FPAIR(4); FPAIR(6);
 #undef FPAIR
-                        if (STG && g == 0) { pk01[0] = pk[0]; pk01[1] = pk[1]; }
+                    };
+#pragma unroll 1
+                    for (uint32_t h = 0; h < 2; h++) { /* two halves of 16 samples, a refill between */
+                        const uint32_t nb = n0 + 16u * h;
+                        group(std::integral_constant<uint32_t, 0>(), nb);
+                        group(std::integral_constant<uint32_t, 1>(), nb + 8u);
+                        if (h == 0) {
+                            if (STG) {
+#pragma unroll
+                                for (int u = 0; u < 4; u++) pk0[u] = pk[u];
+                            } else if (sto) {
+                                nst += 4u * ST_SPG;
+                            }
+                            refill(true); /* the chunk's first half is decoded: n0 + 16 < bs */
+                            st_resync(z0.b, lane);
+                            st_resync(z1.b, lane);
+                        }
                     }
                 };
                 switch (as_fix) {
@@ -3550,18 +3585,18 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                 case 3: chunk(std::integral_constant<int, 3>()); break;
                 default: chunk(std::integral_constant<int, -1>()); break;
                 }
-                z0.left -= ST_CHK;
-                z1.left -= ST_CHK;
+                z0.left -= ST2_CHK;
+                z1.left -= ST2_CHK;
+            } else {
+                refill(false); /* the wave's mid-chunk refill, for this lane's wait */
             }
-            if (!STG && !(ablate & 2u) && any_lane(valid)) nst += (ST_CHK / 4) * ST_SPG;
-
+            if (!STG && sto && any_lane(valid)) nst += 4u * ST_SPG;
         } else {
             STAT(z0.b.stats, 1);
 #pragma unroll 1
-            for (uint32_t g = 0; g < ST_CHK / 8; g++) {
+            for (uint32_t g = 0; g < ST2_CHK / 8; g++) {
                 int32_t L[4], R[4];
                 const uint32_t nb = n0 + g * 8u;
-                const bool sto = !(ablate & 2u);
                 bool st0, st1;
 #define GSTEP(T) st_gen_step<T, FMT>(z0, z1, L, R, limit, trunc, nst, as_uni, as_u, as, dst, nb + T, valid, al, bs, sto)
                 GSTEP(0); GSTEP(1); GSTEP(2);
@@ -3571,32 +3606,42 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                 st1 = GSTEP(7);
                 if (any_lane(st1)) nst += 1u;
 #undef GSTEP
+                if (g == 1) refill(valid && nb + 8u < bs);
             }
         }
         const uint64_t tb = tnow(tmon);
         tm_dec += tb - ta;
-        /* refill before the flush: wait for the previous refill's DMAs (every store since
-         * stays in flight), then issue the next blocks; the flush's stores are younger */
-        {
-            const bool want = valid && n0 + ST_CHK < bs;
-            wait_vm_n(nst);
-            z0.b.vendw = z0.b.iend * 4u;
-            z1.b.vendw = z1.b.iend * 4u;
-            st_refill_issue(z0.b, want);
-            st_refill_issue(z1.b, want);
-            nst = 0;
-        }
+        refill(valid && n0 + ST2_CHK < bs);
         const uint64_t tc = tnow(tmon);
         tm_ref += tc - tb;
-        if (STG && fused) { /* flush: 4 lanes per frame, one 64-byte run each, 16 frames per store */
-            const uint64_t run = (valid && !(ablate & 2u)) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull;
-            u32x4 v[4] = {pk01[0], pk01[1], pk[0], pk[1]};
-            st_quad_transpose(v, podd, phi); /* v[i]: unit (lane & 3) of the quad's frame i */
+        if (STG && fused) {
+            /* flush: every frame's 128-byte run of the chunk as one whole cache line.  Two
+             * rounds of 32 frames through the 4 KB staging tile: the round's lanes write their
+             * eight units (the slot of unit u of frame f is u ^ (f & 7): conflict-free
+             * ds_write_b128), then lane l reads unit l & 7 of frame (l >> 3) + 8 i and stores
+             * it: each store instruction writes 8 whole lines.  Every lane is active here
+             * (a lane whose frame has ended stores nothing: its run address is 0). */
+            const uint64_t run = (valid && sto) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull;
+            const uint32_t rlo = (uint32_t)run, rhi = (uint32_t)(run >> 32);
+            const uint32_t fr = lane & 31u, ul = lane & 7u;
 #pragma unroll
-            for (uint32_t i = 0; i < 4; i++) {
-                const uint64_t a = st_quad_bcast64(run, i);
-                if (a) gst128(a + 16u * fl_unit, v[i]);
-                if (any_lane(a != 0)) nst += 1u;
+            for (uint32_t r = 0; r < 2; r++) {
+                if ((lane >> 5) == r) {
+#pragma unroll
+                    for (uint32_t u = 0; u < 8; u++) lds_st128(stg + fr * 8u + (u ^ (fr & 7u)), u < 4 ? pk0[u] : pk[u - 4]);
+                }
+                lds_sync();
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++) {
+                    const uint32_t f = (lane >> 3) + 8u * i;      /* frame within the round */
+                    const u32x4 v = lds_ld128(stg + f * 8u + (ul ^ (f & 7u)));
+                    const uint32_t src = (32u * r + f) * 4u;     /* its lane, for ds_bpermute */
+                    const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)rhi) << 32) |
+                                       (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)rlo);
+                    lds_sync();
+                    if (a) gst128(a + 16u * ul, v);
+                    if (any_lane(a != 0)) nst += 1u;
+                }
             }
         }
         tm_pack += tnow(tmon) - tc;
