@@ -784,39 +784,6 @@ DEV uint32_t parse_subframe_head(R &b, uint32_t bps, uint32_t bs, uint64_t limit
  * asm one costs a wait state after each), ~30 VALU per step instead of ~55 (round 4). */
 DEV uint32_t ffbh_b(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : ~0u; }
 
-/* The step has no slow-path test of its own: a lane whose first codeword does not fit its
- * window (`stall`) advances nothing, so it stalls again in the next step on the same window;
- * the caller tests the pair's stalls once (skip_stall) */
-DEV void skip_step_ns(BR &b, uint32_t &rem, uint32_t k1, uint32_t km, bool &stall) {
-    const bool live = rem != 0u;
-    const uint32_t w = br_peek(b);
-    const uint32_t q1 = min(ffbh_b(w), 32u);
-    const bool fit1 = live & (q1 <= km);
-    const uint32_t len1 = q1 + k1;
-    const uint32_t q2 = min(ffbh_b(w << (len1 & 31u)), 32u);
-    const uint32_t len2 = len1 + q2 + k1;
-    const bool fit2 = fit1 & (rem >= 2u) & (len2 <= 32u);
-    stall = stall | (live & !fit1);
-    br_adv(b, fit2 ? len2 : (fit1 ? len1 : 0u));
-    rem -= fit2 ? 2u : (fit1 ? 1u : 0u); /* fit2 implies fit1 */
-}
-DEV void skip_stall(BR &b, uint32_t &rem, uint32_t k, uint32_t &p, uint32_t parts, bool &tr, uint64_t limit, bool &stall) {
-    if (__builtin_expect(any_lane(stall), 0)) {
-        if (stall) { /* a unary prefix too long for the window */
-            uint32_t qq;
-            if (br_unary(b, qq, limit)) {
-                br_adv(b, k);
-                rem--;
-            } else { /* truncated: this lane stops walking */
-                tr = true;
-                rem = 0;
-                p = parts;
-            }
-        }
-        stall = false;
-    }
-}
-
 /* Skip the residual of a FIXED/LPC subframe (k_parse's cursor walk).  One loop over the
  * subframe's codewords: a lane whose partition is done reads the next partition header
  * (and skips escaped partitions) on a rare path inside the same loop, so lanes whose
@@ -824,15 +791,51 @@ DEV void skip_stall(BR &b, uint32_t &rem, uint32_t k, uint32_t &p, uint32_t part
  * together instead of waiting for the longest partition of every partition index.  The
  * body is predicated (a lane with nothing left advances 0 bits), and the refill counter is
  * read as a scalar (the wave's lanes step together; it only paces refills every 32
- * codewords).  Returns BNF_ST_TRUNC when the walk runs past the buffer. */
+ * codewords).  Returns BNF_ST_TRUNC when the walk runs past the buffer.
+ * Round 5: the steps move the cursor the way k_decode_st's fused pairs do -- the ring byte
+ * address ra carried along (one carry into the slot bits instead of ring_off per read), the
+ * landing check once per two steps (a step moves wi by at most one word), and the second
+ * codeword's prefix counted in (w << len1) | 1, so no clamp is needed: a window without its
+ * stop bit reads as 31 zeros and the pair does not fit. */
+DEV uint32_t pk_ra(uint32_t wi, uint32_t lane) { return ((wi & 3u) << 2) | (lane << 4) | (((wi >> 2) & 7u) << 10); }
+DEV void pk_resync(BR &b, uint32_t lane) {
+    b.ra = pk_ra(b.wi, lane);
+    b.vlim = b.vendw - 1u;
+}
+DEV void pk_next_word(BR &b) { b.nx = *(const lds_u32 *)((const __attribute__((address_space(3))) uint8_t *)b.ring + b.ra); }
+DEV void pk_step(BR &b, uint32_t &rem, uint32_t k1, bool &stall, uint32_t laneb) {
+    const bool live = rem != 0u;
+    const uint32_t w = br_peek(b);
+    const uint32_t q1 = min(ffbh_b(w), 32u); /* 32 for an empty window: no fit */
+    const uint32_t len1 = q1 + k1;
+    const uint32_t q2 = ffbh_b((w << (len1 & 31u)) | 1u);
+    const uint32_t len2 = len1 + q2 + k1; /* both codewords: fits iff <= 32 (and the first fits) */
+    const bool fit1 = live & (len1 <= 32u);
+    const bool fit2 = fit1 & (rem >= 2u) & (len2 <= 32u);
+    stall = stall | (live & !fit1);
+    const uint32_t n = fit2 ? len2 : (fit1 ? len1 : 0u);
+    rem -= fit2 ? 2u : (fit1 ? 1u : 0u);
+    uint32_t t;
+    const bool c = __builtin_usub_overflow(b.s, n, &t); /* the window moves on a word */
+    b.s = t & 31u;
+    b.hi = c ? b.lo : b.hi;
+    b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
+    b.wi += (uint32_t)c;
+    b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x1C0Cu) | laneb;
+}
 DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate) {
     const uint32_t parts = 1u << h.porder;
     const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
     const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
-    uint32_t since = 0, p = 0, rem = 0, k = 0, k1 = 1, km = 31;
+    const uint32_t lane = threadIdx.x & 63u, laneb = lane << 4;
+    uint32_t since = 0, p = 0, rem = 0, k = 0, k1 = 1;
     bool tr = false;
+    pk_resync(b, lane);
     while (any_lane(rem != 0u || p < parts)) {
-        if ((__builtin_amdgcn_readfirstlane(since++) & 7u) == 0u && !(ablate & 32u)) br_refill(b);
+        if ((__builtin_amdgcn_readfirstlane(since++) & 7u) == 0u && !(ablate & 32u)) {
+            br_refill(b);
+            pk_resync(b, lane);
+        }
         const bool sw = rem == 0u && p < parts;
         if (__builtin_expect(any_lane(sw), 0)) { /* partition headers (read_residual_partitioned_rice_ @0x10012da0) */
             if (sw) {
@@ -851,19 +854,38 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
                     } else {
                         k = kk;
                         k1 = kk + 1u;
-                        km = 31u - kk;
                         rem = cnt; /* 0: the empty first partition (order == partition size) */
                     }
                 } while (rem == 0u && p < parts);
             }
+            pk_resync(b, lane);
         }
         /* two steps per switch test (a lane that finishes its partition in the first one
-         * idles in the second) and per slow-path test */
-        {
-            bool stall = false;
-            skip_step_ns(b, rem, k1, km, stall);
-            skip_step_ns(b, rem, k1, km, stall);
-            skip_stall(b, rem, k, p, parts, tr, limit, stall);
+         * idles in the second), per landing check and per slow-path test */
+        bool stall = false;
+        pk_step(b, rem, k1, stall, laneb);
+        const bool ld = b.wi >= b.vlim; /* word wi + 1 (the next step's read) not known to have landed */
+        pk_next_word(b);
+        if (__builtin_expect(any_lane(ld), 0)) {
+            br_land(b, 1u);
+            pk_resync(b, lane);
+            pk_next_word(b);
+        }
+        pk_step(b, rem, k1, stall, laneb);
+        pk_next_word(b);
+        if (__builtin_expect(any_lane(stall), 0)) {
+            if (stall) { /* a unary prefix too long for the window */
+                uint32_t qq;
+                if (br_unary(b, qq, limit)) {
+                    br_adv(b, k);
+                    rem--;
+                } else { /* truncated: this lane stops walking */
+                    tr = true;
+                    rem = 0;
+                    p = parts;
+                }
+            }
+            pk_resync(b, lane);
         }
     }
     return (tr || br_pos(b) > limit) ? BNF_ST_TRUNC : BNF_ST_OK;
