@@ -523,8 +523,16 @@ def leg(cfg, args, torch, dev, libflac, synth, dec, stream):
         r = c5_job(args, torch, None, dev, libflac, synth, dec, 1, 0, files=c["batches"], steps=args.leg_steps,
                    warmup=1)
         out = c5_summary(r, args, 1, steps=args.leg_steps)
-        for k in ("with_gather", "with_gather_overlapped", "ranks"):
+        for k in ("with_gather", "with_gather_overlapped", "with_gather_in_step", "ranks"):
             out.pop(k, None)
+        # one file: the per-rank work of C5 at N = 8 (one file per GPU), and what it implies
+        r1 = c5_job(args, torch, None, dev, libflac, synth, dec, 1, 0, files=1, steps=args.leg_steps, warmup=1)
+        one_ms = r1["t_dec"] / args.leg_steps * 1e3
+        out["one_file"] = {"ms_per_step": round(one_ms, 4), "parse_ms": round(r1["t_parse"], 4),
+                           "decode_ms": round(r1["t_decode"], 4), "bitexact": r1["ok"],
+                           "projected_8gpu_speedup": round(out["ms_per_step"] / one_ms, 3),
+                           "note": "PROJECTION, not a measurement of 8 GPUs: one file's step on this GPU is each "
+                                   "rank's work at N = 8; speedup = the 8-file step here / that (gather excluded)"}
         out["steps"] = args.leg_steps
         out["config"] = {"workload": c["desc"], "files": r["files"], "frames_per_step": r["frames_rank"]}
         if not args.no_cpu_baseline:
@@ -658,10 +666,38 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank, files=None,
         last = (steps - 1) % 2
         if rank == 0 and parts[last] is not None:
             gathered_ovl = torch.cat(parts[last])
+    # decode + gather overlapped inside one step: the rank's files decoded one
+    # group (file) at a time, each group's PCM posted to rank 0 (shard.GroupGather) as soon as
+    # its decode is enqueued, so group g's transfer runs beside group g + 1's decode
+    t_grp, gathered_grp = t_all, None
     if world > 1:
-        t = torch.tensor([t_dec, t_all, t_ovl], dtype=torch.float64, device=dev)
+        fb = [0] + list(np.cumsum([len(o) for o in offs]))          # frame range of each file
+        sb = [0] + list(np.cumsum([s.nsamples * stride for s in streams]))  # its byte range in d_out
+        gsz = shard.gather_group_sizes([int(sb[i + 1] - sb[i]) for i in range(len(streams))], device=dev)
+
+        def grouped():
+            gg = shard.GroupGather(gsz, d_out)
+            for i in range(len(streams)):
+                f0, f1 = int(fb[i]), int(fb[i + 1])
+                di = d_info[f0 * libflac.FRAME_INFO_BYTES:f1 * libflac.FRAME_INFO_BYTES]
+                dec.parse_frames(d_bytes, nb, d_offs[f0:f1], f1 - f0, sp, di, d_out_sample=d_os[f0:f1], stream=stream)
+                dec.decode_parsed(d_bytes, nb, f1 - f0, sp, fmt, d_out, di, stream=stream)
+                gg.post(i, d_out[int(sb[i]):int(sb[i + 1])])
+            return gg.wait()
+
+        grouped()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            gathered_grp = grouped()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t_grp = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([t_dec, t_all, t_ovl, t_grp], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_dec, t_all, t_ovl = float(t[0].item()), float(t[1].item()), float(t[2].item())
+        t_dec, t_all, t_ovl, t_grp = float(t[0].item()), float(t[1].item()), float(t[2].item()), float(t[3].item())
     ok = True
     if rank == 0:
         local = dict(zip(mine, streams))
@@ -670,6 +706,7 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank, files=None,
         ok = gathered is not None and gathered.cpu().numpy().tobytes() == ref
         if world > 1:
             ok = ok and gathered_ovl is not None and gathered_ovl.cpu().numpy().tobytes() == ref
+            ok = ok and gathered_grp is not None and gathered_grp.cpu().numpy().tobytes() == ref
     if world > 1:
         o = torch.tensor([1 if ok else 0], device=dev)
         dist.all_reduce(o, op=dist.ReduceOp.MIN)
@@ -681,7 +718,7 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank, files=None,
     samples = int(tot.item())
     comp = sum(len(s.data) - int(s.frame_offsets[0]) for s in streams)
     alg = comp + nsmp * stride
-    return {"samples": samples, "t_dec": t_dec, "t_all": t_all, "t_ovl": t_ovl, "t_launch": t_launch, "ok": ok,
+    return {"samples": samples, "t_dec": t_dec, "t_all": t_all, "t_ovl": t_ovl, "t_grp": t_grp, "t_launch": t_launch, "ok": ok,
             "t_parse": t_parse, "t_decode": t_decode,
             "files": F, "alg_bytes_rank": alg, "frames_rank": nframes}
 
@@ -701,7 +738,12 @@ def c5_summary(r, args, world, steps=None):
            "with_gather_overlapped": {"value": round(r["samples"] * steps / r["t_ovl"] / 1e6, 2),
                                       "unit": "MSamples/s", "ms_per_step": round(r["t_ovl"] / steps * 1e3, 4),
                                       "note": "step s's gather (shard.gather_post, RCCL send/recv) in flight while "
-                                              "step s + 1 decodes into a second buffer; N = 1: no gather"}}
+                                              "step s + 1 decodes into a second buffer; N = 1: no gather"},
+           "with_gather_in_step": {"value": round(r["samples"] * steps / r["t_grp"] / 1e6, 2),
+                                   "unit": "MSamples/s", "ms_per_step": round(r["t_grp"] / steps * 1e3, 4),
+                                   "note": "one step: the rank's files decoded one at a time, each file's PCM "
+                                           "posted to rank 0 (shard.GroupGather) as soon as its decode is "
+                                           "enqueued; N = 1: no gather"}}
     out["roofline"]["kernel"] = "decode launch over the rank's files (k_parse beside it: k_parse_avg_ms)"
     out["roofline"]["parse_plus_decode_ms"] = round(r["t_launch"], 4)
     return out

@@ -3653,16 +3653,22 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                     for (uint32_t u = 0; u < 8; u++) lds_st128(stg + fr * 8u + (u ^ (fr & 7u)), u < 4 ? pk0[u] : pk[u - 4]);
                 }
                 lds_sync();
+                /* the round's four units and run addresses, one wait for all of them */
+                u32x4 v[4];
+                uint64_t a[4];
 #pragma unroll
                 for (uint32_t i = 0; i < 4; i++) {
                     const uint32_t f = (lane >> 3) + 8u * i;      /* frame within the round */
-                    const u32x4 v = lds_ld128(stg + f * 8u + (ul ^ (f & 7u)));
+                    v[i] = lds_ld128(stg + f * 8u + (ul ^ (f & 7u)));
                     const uint32_t src = (32u * r + f) * 4u;     /* its lane, for ds_bpermute */
-                    const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)rhi) << 32) |
-                                       (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)rlo);
-                    lds_sync();
-                    if (a) gst128(a + 16u * ul, v);
-                    if (any_lane(a != 0)) nst += 1u;
+                    a[i] = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)rhi) << 32) |
+                           (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)rlo);
+                }
+                lds_sync();
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++) {
+                    if (a[i]) gst128(a[i] + 16u * ul, v[i]);
+                    if (any_lane(a[i] != 0)) nst += 1u;
                 }
             }
         }

@@ -107,3 +107,88 @@ def gather_post(local, sizes, group=None, dst: int = 0, parts=None):
     if local.numel():
         return dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), glob(dst), group)]), None
     return [], None
+
+
+def gather_group_sizes(group_sizes, group=None, device=None):
+    """Every rank's per-group byte counts (all_gather of a fixed-width int64 vector, padded
+    with -1), for GroupGather: a rank's output is the concatenation of its groups.  device:
+    where the collective's tensors live (the GPU under RCCL, the CPU under gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    n = torch.tensor([len(group_sizes)], dtype=torch.int64, device=device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    width = max(int(x.item()) for x in ns)
+    mine = torch.full((max(width, 1),), -1, dtype=torch.int64, device=device)
+    if len(group_sizes):
+        mine[:len(group_sizes)] = torch.tensor(list(group_sizes), dtype=torch.int64, device=device)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine, group=group)
+    return [[int(v) for v in a.tolist() if v >= 0] for a in allv]
+
+
+class GroupGather:
+    """A gather of every rank's output to `dst` that starts while the ranks are still decoding
+    ("overlap the gather chunk-wise with decode").  A rank decodes its
+    files in groups into consecutive slices of its output buffer and calls post(g, slice) as
+    soon as group g is enqueued; `dst` posted every receive up front, straight into the final
+    buffer at the rank-major, group-minor offset, so nothing is concatenated afterwards.
+    Under RCCL each post runs on the communicator's stream after the work already enqueued on
+    the current stream (that group's decode) and beside the decode of the next group; per
+    peer, sends and receives match in group order.  wait() completes everything; on `dst`
+    `out` then holds all ranks' bytes in rank order."""
+
+    def __init__(self, sizes, like, group=None, dst: int = 0, out=None):
+        import torch
+        import torch.distributed as dist
+
+        self.dist, self.group, self.dst = dist, group, dst
+        self.rank = dist.get_rank(group)
+        world = dist.get_world_size(group)
+        self.glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
+        self.sizes = sizes
+        self.works = []
+        self.order = []  # (rank, group) of every post made by this rank, in post order
+        self.out = None
+        if self.rank == dst:
+            total = sum(sum(s) for s in sizes)
+            self.out = out if out is not None else torch.empty(total, dtype=like.dtype, device=like.device)
+            self.base = []
+            off = 0
+            for r in range(world):
+                row = []
+                for s in sizes[r]:
+                    row.append(off)
+                    off += s
+                self.base.append(row)
+            ops = []
+            for r in range(world):
+                if r == self.rank:
+                    continue
+                for g, s in enumerate(sizes[r]):
+                    if s:
+                        ops.append(dist.P2POp(dist.irecv, self.out[self.base[r][g]:self.base[r][g] + s], self.glob(r), group))
+                        self.order.append(("recv", r, g))
+            if ops:
+                self.works += dist.batch_isend_irecv(ops)
+
+    def post(self, g, part):
+        """Group g of this rank (its bytes, in this rank's output order) is enqueued: send it
+        (or, on `dst`, copy it into place)."""
+        if self.rank == self.dst:
+            if part.numel():
+                self.out[self.base[self.rank][g]:self.base[self.rank][g] + part.numel()].copy_(part, non_blocking=True)
+            self.order.append(("copy", self.rank, g))
+            return
+        if part.numel():
+            self.works += self.dist.batch_isend_irecv([self.dist.P2POp(self.dist.isend, part.contiguous(),
+                                                                       self.glob(self.dst), self.group)])
+        self.order.append(("send", self.rank, g))
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+        return self.out

@@ -167,3 +167,56 @@ def test_overlapped_gather_pipeline(world):
     ref = b"".join(torch.arange(1000 + 37 * r, dtype=torch.int64).add(r * 7 + st * 13).remainder(251).to(torch.uint8)
                    .numpy().tobytes() for r in range(world))
     assert got == ref
+
+
+def _group_worker(rank, world, port, groups, result_q):
+    """One rank "decodes" its files in groups (bytes derived from rank, group and position) and
+    posts each group as soon as it is written; rank 0 checks the gathered bytes and the post
+    order (receives posted first, then this rank's groups in decode order)."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = groups[rank]
+        out = torch.zeros(sum(mine), dtype=torch.uint8)
+        sizes = shard.gather_group_sizes(mine)
+        assert sizes == groups
+        gg = shard.GroupGather(sizes, out)
+        off = 0
+        for g, n in enumerate(mine):
+            part = out[off:off + n]
+            part.copy_(torch.arange(n, dtype=torch.int64).add(rank * 31 + g * 7).remainder(253).to(torch.uint8))
+            gg.post(g, part)
+            off += n
+        got = gg.wait()
+        if rank == 0:
+            result_q.put((got.numpy().tobytes(), gg.order))
+        else:
+            assert got is None
+            assert gg.order == [("send", rank, g) for g in range(len(mine))]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_group_gather_overlaps_decode_three_ranks():
+    """shard.GroupGather (the C5 flow's in-job overlap): every rank posts its groups as they
+    are decoded; rank 0 has every receive posted up front, into the final buffer at the
+    rank-major, group-minor offsets.  Ragged groups, an empty group, a rank with one group."""
+    import torch.multiprocessing as mp
+    groups = [[300, 0, 1201], [4096, 17], [999]]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, 3, port, groups, q)) for r in range(3)]
+    for pr in procs:
+        pr.start()
+    got, order = q.get(timeout=120)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    want = b"".join(bytes((i + r * 31 + g * 7) % 253 for i in range(n)) for r, gs in enumerate(groups)
+                    for g, n in enumerate(gs))
+    assert got == want
+    assert order == [("recv", 1, 0), ("recv", 1, 1), ("recv", 2, 0), ("copy", 0, 0), ("copy", 0, 1), ("copy", 0, 2)]
