@@ -213,6 +213,14 @@ DEV void lds_dma16(const void *g, lds_u32 *dst) {
 DEV void dma_block(const BR &b, uint32_t j, uint32_t slot) { /* one 16-byte block per lane */
     lds_dma16(b.w + (uint64_t)min(j, b.nblk - 1u) * 4u, b.ring + slot * RING_LANE_DW);
 }
+/* The same with the instruction's immediate offset (one address for consecutive blocks).  The
+ * offset moves the LDS destination as well as the global address (measured on gfx950,
+ * tools/dbg_glds_off.hip), so the LDS base passed is the slot row minus the offset: the
+ * row still receives lane l's 16 bytes at +16 l. */
+template <int OFF>
+DEV void lds_dma16_off(const void *g, lds_u32 *row) {
+    __builtin_amdgcn_global_load_lds((gvoid *)g, (lds_void *)(row - OFF / 4), 16, OFF, 0);
+}
 
 /* Issue the blocks this lane will need next (exec-masked LDS-DMA per ring slot).  Blocks
  * issued earlier have landed once the wait returns.  The block of word wi is kept: br_adv
@@ -823,16 +831,42 @@ DEV void pk_step(BR &b, uint32_t &rem, uint32_t k1, bool &stall, uint32_t laneb)
     b.wi += (uint32_t)c;
     b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x1C0Cu) | laneb;
 }
-DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate) {
+/* The bulk step: two codewords of a lane that has plenty left in its partition, nothing but
+ * the fit test (nf counts the steps whose pair did not fit: the lane did not move, and it
+ * stays put for the iteration's remaining steps, as they see the same window).  (w | 1) keeps
+ * the count finite; an empty window reads as 31 zeros, which cannot fit. */
+DEV void pkb_step(BR &b, uint32_t k1, uint32_t &nf, uint32_t laneb) {
+    const uint32_t w = br_peek(b);
+    const uint32_t len1 = (uint32_t)__builtin_clz(w | 1u) + k1;
+    const uint32_t n = len1 + (uint32_t)__builtin_clz((w << (len1 & 31u)) | 1u) + k1;
+    const bool fit = n <= 32u;
+    nf += fit ? 0u : 1u;
+    uint32_t t;
+    const bool c = __builtin_usub_overflow(b.s, fit ? n : 0u, &t);
+    b.s = t & 31u;
+    b.hi = c ? b.lo : b.hi;
+    b.lo = c ? __builtin_bswap32(b.nx) : b.lo;
+    b.wi += (uint32_t)c;
+    b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x1C0Cu) | laneb;
+}
+template <bool BULK> /* BULK: with the bulk iterations (a separate instance: the plain loop keeps its registers) */
+DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate) {
     const uint32_t parts = 1u << h.porder;
     const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
     const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
     const uint32_t lane = threadIdx.x & 63u, laneb = lane << 4;
-    uint32_t since = 0, p = 0, rem = 0, k = 0, k1 = 1;
+    uint32_t since = BULK ? 16u : 0u, p = 0, rem = 0, k = 0, k1 = 1;
     bool tr = false;
     pk_resync(b, lane);
     while (any_lane(rem != 0u || p < parts)) {
-        if ((__builtin_amdgcn_readfirstlane(since++) & 7u) == 0u && !(ablate & 32u)) {
+        if (BULK) {
+            if (__builtin_amdgcn_readfirstlane(since) >= 12u && !(ablate & 32u)) { /* every 12-14 steps */
+                br_refill(b);
+                pk_resync(b, lane);
+                since = 0;
+            }
+            since += 2u;
+        } else if ((__builtin_amdgcn_readfirstlane(since++) & 7u) == 0u && !(ablate & 32u)) { /* every 16 steps */
             br_refill(b);
             pk_resync(b, lane);
         }
@@ -860,6 +894,51 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
             }
             pk_resync(b, lane);
         }
+        /* bulk iterations: every lane has 8+ codewords left in its partition and a Rice
+         * parameter whose pairs mostly fit one window (C2: all but the partition ends) --
+         * four pair steps with the landing check after the first and third; at most three
+         * per outer iteration, so one refill paces both (at most 14 steps apart). */
+#pragma unroll 1
+        for (uint32_t it = 0; BULK && it < 3u && !any_lane(rem < 8u || k1 > 10u); it++) {
+            uint32_t nf = 0;
+            pkb_step(b, k1, nf, laneb);
+            bool ld = b.wi >= b.vlim;
+            pk_next_word(b);
+            if (__builtin_expect(any_lane(ld), 0)) {
+                br_land(b, 1u);
+                pk_resync(b, lane);
+                pk_next_word(b);
+            }
+            pkb_step(b, k1, nf, laneb);
+            pk_next_word(b);
+            pkb_step(b, k1, nf, laneb);
+            ld = b.wi >= b.vlim;
+            pk_next_word(b);
+            if (__builtin_expect(any_lane(ld), 0)) {
+                br_land(b, 1u);
+                pk_resync(b, lane);
+                pk_next_word(b);
+            }
+            pkb_step(b, k1, nf, laneb);
+            pk_next_word(b);
+            rem -= 8u - 2u * nf;
+            since += 4u;
+            if (__builtin_expect(any_lane(nf != 0u), 0)) {
+                if (nf) { /* a pair that did not fit: its first codeword alone, generic reader */
+                    uint32_t qq;
+                    if (br_unary(b, qq, limit)) {
+                        br_adv(b, k);
+                        rem--;
+                    } else {
+                        tr = true;
+                        rem = 0;
+                        p = parts;
+                    }
+                }
+                pk_resync(b, lane);
+            }
+        }
+        if (BULK && !any_lane(rem != 0u || p < parts)) break;
         /* two steps per switch test (a lane that finishes its partition in the first one
          * idles in the second), per landing check and per slow-path test */
         bool stall = false;
@@ -889,6 +968,14 @@ DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, 
         }
     }
     return (tr || br_pos(b) > limit) ? BNF_ST_TRUNC : BNF_ST_OK;
+}
+/* The bulk instance when every lane's first partition has a small Rice parameter (k <= 9:
+ * pairs of codewords fit a window; C2's k = 8), peeked at the cursor, which sits on that
+ * parameter; the plain loop otherwise (C3 / C4: larger parameters, short partitions). */
+DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate) {
+    const uint32_t k0 = br_peek(b) >> (h.rice2 ? 27u : 28u);
+    if (!any_lane(k0 > 9u)) return skip_residual_t<true>(b, h, bs, limit, ablate);
+    return skip_residual_t<false>(b, h, bs, limit, ablate);
 }
 
 /* ------------------------------------------- wave-cooperative Rice boundary scan */
@@ -3115,6 +3202,36 @@ DEV void st_decor4t(bool uni, uint32_t as_u, uint32_t as, int32_t (&L)[4], int32
     }
 }
 
+/* Decorrelation of two consecutive samples of both channels straight from the packed history
+ * pairs (a: channel 0's, b: channel 1's; low half the later sample), in 16-bit lanes: the
+ * FLACDecoder/FLACFileReader 16-bit layouts keep the low 16 bits of L and R, and every
+ * operation here is exact mod 2^16 (M/S: ceil(S/2) = S - (S >> 1) stays within int16). */
+typedef unsigned short st_u2 __attribute__((ext_vector_type(2)));
+typedef short st_i2 __attribute__((ext_vector_type(2)));
+template <int AS>
+DEV void st_pair_lr(uint32_t a, uint32_t b, uint32_t &l, uint32_t &r) {
+    const st_u2 x = __builtin_bit_cast(st_u2, a), y = __builtin_bit_cast(st_u2, b);
+    st_u2 L = x, R = y;
+    if (AS == 1) R = x - y;
+    else if (AS == 2) L = x + y;
+    else if (AS == 3) {
+        const st_u2 h = y - __builtin_bit_cast(st_u2, __builtin_bit_cast(st_i2, b) >> (st_i2){1, 1});
+        L = x + h;
+        R = L - y;
+    }
+    l = __builtin_bit_cast(uint32_t, L);
+    r = __builtin_bit_cast(uint32_t, R);
+}
+/* the four 16-bit L | R << 16 words of samples n-3..n from the pairs (n-3, n-2) and (n-1, n) */
+template <int AS>
+DEV u32x4 st_pack4(uint32_t a01, uint32_t b01, uint32_t a23, uint32_t b23) {
+    uint32_t l01, r01, l23, r23;
+    st_pair_lr<AS>(a01, b01, l01, r01);
+    st_pair_lr<AS>(a23, b23, l23, r23);
+    return u32x4{__builtin_amdgcn_perm(r01, l01, 0x07060302u), __builtin_amdgcn_perm(r01, l01, 0x05040100u),
+                 __builtin_amdgcn_perm(r23, l23, 0x07060302u), __builtin_amdgcn_perm(r23, l23, 0x05040100u)};
+}
+
 /* Pack and store samples n..n+3 of this lane's frame (nv of them valid); returns whether
  * this lane issued a store.  dst: the frame's first byte in the layout (planar: channel 0). */
 template <int FMT>
@@ -3161,13 +3278,25 @@ DEV void st_refill_issue(BR &b, bool want) {
     const uint32_t cg = (b.wi >> 2) & ~3u; /* first block of the cursor's group */
     const bool go = want && b.iend == cg + 4u;
     const uint32_t h = b.iend & 4u; /* the free group's slots: 0-3 or 4-7 */
+    /* a group wholly inside the buffer: one address, the four blocks by immediate offset
+     * (round 5: ~20 fewer VALU per refill and channel); the buffer's last blocks clamped */
+    const bool whole = b.iend + 3u < b.nblk;
+    const uint32_t *a = b.w + (uint64_t)b.iend * 4u;
 #pragma unroll
     for (int g = 0; g < 2; g++) {
         const bool gg = go && h == 4u * (uint32_t)g;
         if (__any(gg)) {
             if (gg) {
+                lds_u32 *row = b.ring + 4u * (uint32_t)g * RING_LANE_DW;
+                if (__builtin_expect(whole, 1)) {
+                    lds_dma16_off<0>(a, row);
+                    lds_dma16_off<16>(a, row + RING_LANE_DW);
+                    lds_dma16_off<32>(a, row + 2 * RING_LANE_DW);
+                    lds_dma16_off<48>(a, row + 3 * RING_LANE_DW);
+                } else {
 #pragma unroll
-                for (int k = 0; k < 4; k++) dma_block(b, b.iend + (uint32_t)k, 4u * (uint32_t)g + (uint32_t)k);
+                    for (int k = 0; k < 4; k++) dma_block(b, b.iend + (uint32_t)k, 4u * (uint32_t)g + (uint32_t)k);
+                }
             }
         }
     }
@@ -3350,6 +3479,10 @@ DEV void st_lpc_out(StCh &z0, StCh &z1, uint32_t u0, uint32_t u1, int32_t (&L)[4
                 R[q] = (int32_t)((uint32_t)R[q] << z1.wasted);
             }
         }
+        if (STG && AS >= 0) { /* no wasted bits: the history pairs hold the samples */
+            pk[PO + (T >> 2)] = st_pack4<AS>(z0.q[(T + 6) & 7], z1.q[(T + 6) & 7], z0.q[T], z1.q[T]);
+            return;
+        }
         st_decor4t<AS>(as_uni, as_u, as, L, R);
         if (STG) {
             uint32_t w[4];
@@ -3364,15 +3497,16 @@ DEV void st_lpc_out(StCh &z0, StCh &z1, uint32_t u0, uint32_t u1, int32_t (&L)[4
 
 /* Two Rice codewords of one channel from one 32-bit window (the pair fits when their lengths
  * sum to <= 32: always at C2's parameters, k = 8 and ~10-bit codewords).  The second's prefix
- * is counted in the window shifted past the first; ffbh of an all-zero window is clamped to
- * 32 so a prefix that runs off the window always reads as not fitting.  Returns the bits
+ * is counted in the window shifted past the first; the prefix counts are taken of (x | 1), so
+ * a prefix that runs off the window reads as 31 zeros and the pair as not fitting (a fast
+ * v_or instead of a clamp after the count, round 5).  Returns the bits
  * both take, or 0 with sl set (the lane then decodes the two with the generic reader). */
 DEV uint32_t st_rice_pair(const StCh &z, uint32_t &ua, uint32_t &ub, bool &sl) {
     const uint32_t w = br_peek(z.b);
-    const uint32_t qa = min(ffbh(w), 32u);
+    const uint32_t qa = (uint32_t)__builtin_clz(w | 1u); /* 31 for an empty window: n > 32 below */
     const uint32_t la = qa + z.k1;
-    const uint32_t w2 = w << (la & 31u); /* la == 32: garbage, and n > 32 below */
-    const uint32_t qb = min(ffbh(w2), 32u);
+    const uint32_t w2 = w << (la & 31u); /* la >= 32: garbage, and n > 32 below */
+    const uint32_t qb = (uint32_t)__builtin_clz(w2 | 1u);
     ua = (qa << z.k) | __builtin_amdgcn_ubfe(w, z.km - qa, z.k);
     ub = (qb << z.k) | __builtin_amdgcn_ubfe(w2, z.km - qb, z.k);
     const uint32_t n = la + qb + z.k1;
