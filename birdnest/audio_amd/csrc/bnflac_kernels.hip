@@ -1787,6 +1787,69 @@ DEV uint32_t crc16_shift(uint32_t crc, uint64_t nbytes) {
     return crc;
 }
 
+/* CRC-16 of [b0, b1) with two 64-byte loads in flight (g_crc16_t11 tables in LDS: 0.75
+ * lookups per byte on whole lines, the byte table on the unaligned ends) */
+DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line offset o: bytes below h cleared */
+    return h <= o ? ~0u : (h >= o + 4u ? 0u : (~0u << (8u * (h - o))));
+}
+#define CRC_LINES 4
+DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
+    uint32_t crc = 0; /* byte-swapped until the trailing bytes (crc16_step8le) */
+    /* whole lines from the one holding b0, its bytes below b0 taken as zeros (a CRC with
+     * init 0 stays 0 over leading zero bytes) */
+    const uint64_t p0 = b0 & ~(uint64_t)63u;
+    const uint32_t h = (uint32_t)(b0 & 63u);
+    const uint32_t nl = b1 > p0 ? (uint32_t)((b1 - p0) >> 6) : 0u;
+    uint64_t p = b0;
+    if (nl) {
+        /* CRC_LINES lines in flight per lane: each lane walks its own frame, so the loads of
+         * one line wait a full HBM latency; one line ahead left the loop latency-bound */
+        const uint4 *q = (const uint4 *)(bytes + p0);
+        uint4 buf[CRC_LINES][4];
+#pragma unroll
+        for (int d = 0; d < CRC_LINES; d++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) buf[d][u] = q[4u * min((uint32_t)d, nl - 1u) + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            buf[0][u].x &= st_hmask(h, 16u * u);
+            buf[0][u].y &= st_hmask(h, 16u * u + 4u);
+            buf[0][u].z &= st_hmask(h, 16u * u + 8u);
+            buf[0][u].w &= st_hmask(h, 16u * u + 12u);
+        }
+        for (uint32_t i = 0; i < nl; i += CRC_LINES) {
+#pragma unroll
+            for (int d = 0; d < CRC_LINES; d++) {
+                if (i + d < nl) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        crc = crc16_step8le(crc, buf[d][u].x, buf[d][u].y, T);
+                        crc = crc16_step8le(crc, buf[d][u].z, buf[d][u].w, T);
+                    }
+                    const uint32_t j = min(i + d + CRC_LINES, nl - 1u);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) buf[d][u] = q[4u * j + u];
+                }
+            }
+        }
+        p = p0 + (uint64_t)nl * 64u;
+        /* the last partial line: whole 8-byte steps (loads issued together), then bytes */
+        const uint32_t n8 = (uint32_t)((b1 - p) >> 3);
+        const uint2 *q8 = (const uint2 *)(bytes + p);
+        uint2 t8[7];
+#pragma unroll
+        for (uint32_t i = 0; i < 7; i++) t8[i] = i < n8 ? q8[i] : make_uint2(0u, 0u);
+#pragma unroll
+        for (uint32_t i = 0; i < 7; i++)
+            if (i < n8) crc = crc16_step8le(crc, t8[i].x, t8[i].y, T);
+        p += 8u * n8;
+    }
+    crc = crc16_unswap(crc);
+    /* trailing bytes: the byte table is w1's [22,32) field table at byte << 2 (stream byte 7) */
+    while (p < b1) { crc = ((crc << 8) ^ crc16_unswap(T[CRC11_W1F2 + ((((crc >> 8) ^ bytes[p]) & 0xffu) << 2)])) & 0xffff; p++; }
+    return crc;
+}
+
 /* Wave-cooperative CRC-16 of one byte range (the whole wave, coalesced 1 KB loads).
  * Layout: 16-byte pieces counted back from e = round_up(b1, 16); lane l takes pieces
  * 63 - l + 64 m, so every wave load is 64 consecutive pieces.  Each lane runs a CRC over
@@ -1868,6 +1931,8 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
     parse_frame(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
                 (perm && slot < nframes) ? perm[slot] : slot);
 }
+
+
 
 /* =========================================================== k_parse_wave
  * One wave per frame: the same record as parse_frame (header, subframe starts, decode class),
@@ -3274,7 +3339,7 @@ DEV bool st_emit4(uint8_t *dst, uint32_t n, uint32_t nv, bool al, uint32_t bs, c
  * refill costs a line fetch from the fabric.  A group fetched now lands before the next
  * refill's wait; the cursor needs it only after the ~64 bytes of the current group.
  * Whole wave: exec-masked, and only the slot groups some lane needs are issued. */
-DEV void st_refill_issue(BR &b, bool want) {
+DEV uint32_t st_refill_issue(BR &b, bool want) { /* returns a lower bound of the DMA instructions issued */
     const uint32_t cg = (b.wi >> 2) & ~3u; /* first block of the cursor's group */
     const bool go = want && b.iend == cg + 4u;
     const uint32_t h = b.iend & 4u; /* the free group's slots: 0-3 or 4-7 */
@@ -3282,10 +3347,12 @@ DEV void st_refill_issue(BR &b, bool want) {
      * (round 5: ~20 fewer VALU per refill and channel); the buffer's last blocks clamped */
     const bool whole = b.iend + 3u < b.nblk;
     const uint32_t *a = b.w + (uint64_t)b.iend * 4u;
+    uint32_t nd = 0;
 #pragma unroll
     for (int g = 0; g < 2; g++) {
         const bool gg = go && h == 4u * (uint32_t)g;
         if (__any(gg)) {
+            nd += 4u;
             if (gg) {
                 lds_u32 *row = b.ring + 4u * (uint32_t)g * RING_LANE_DW;
                 if (__builtin_expect(whole, 1)) {
@@ -3301,70 +3368,9 @@ DEV void st_refill_issue(BR &b, bool want) {
         }
     }
     if (go) b.iend += 4u;
+    return nd;
 }
 
-/* CRC-16 of [b0, b1) with two 64-byte loads in flight (g_crc16_t11 tables in LDS: 0.75
- * lookups per byte on whole lines, the byte table on the unaligned ends) */
-DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line offset o: bytes below h cleared */
-    return h <= o ? ~0u : (h >= o + 4u ? 0u : (~0u << (8u * (h - o))));
-}
-#define CRC_LINES 4
-DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
-    uint32_t crc = 0; /* byte-swapped until the trailing bytes (crc16_step8le) */
-    /* whole lines from the one holding b0, its bytes below b0 taken as zeros (a CRC with
-     * init 0 stays 0 over leading zero bytes) */
-    const uint64_t p0 = b0 & ~(uint64_t)63u;
-    const uint32_t h = (uint32_t)(b0 & 63u);
-    const uint32_t nl = b1 > p0 ? (uint32_t)((b1 - p0) >> 6) : 0u;
-    uint64_t p = b0;
-    if (nl) {
-        /* CRC_LINES lines in flight per lane: each lane walks its own frame, so the loads of
-         * one line wait a full HBM latency; one line ahead left the loop latency-bound */
-        const uint4 *q = (const uint4 *)(bytes + p0);
-        uint4 buf[CRC_LINES][4];
-#pragma unroll
-        for (int d = 0; d < CRC_LINES; d++)
-#pragma unroll
-            for (int u = 0; u < 4; u++) buf[d][u] = q[4u * min((uint32_t)d, nl - 1u) + u];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            buf[0][u].x &= st_hmask(h, 16u * u);
-            buf[0][u].y &= st_hmask(h, 16u * u + 4u);
-            buf[0][u].z &= st_hmask(h, 16u * u + 8u);
-            buf[0][u].w &= st_hmask(h, 16u * u + 12u);
-        }
-        for (uint32_t i = 0; i < nl; i += CRC_LINES) {
-#pragma unroll
-            for (int d = 0; d < CRC_LINES; d++) {
-                if (i + d < nl) {
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        crc = crc16_step8le(crc, buf[d][u].x, buf[d][u].y, T);
-                        crc = crc16_step8le(crc, buf[d][u].z, buf[d][u].w, T);
-                    }
-                    const uint32_t j = min(i + d + CRC_LINES, nl - 1u);
-#pragma unroll
-                    for (int u = 0; u < 4; u++) buf[d][u] = q[4u * j + u];
-                }
-            }
-        }
-        p = p0 + (uint64_t)nl * 64u;
-        /* the last partial line: whole 8-byte steps (loads issued together), then bytes */
-        const uint32_t n8 = (uint32_t)((b1 - p) >> 3);
-        const uint2 *q8 = (const uint2 *)(bytes + p);
-        uint2 t8[7];
-#pragma unroll
-        for (uint32_t i = 0; i < 7; i++) t8[i] = i < n8 ? q8[i] : make_uint2(0u, 0u);
-#pragma unroll
-        for (uint32_t i = 0; i < 7; i++)
-            if (i < n8) crc = crc16_step8le(crc, t8[i].x, t8[i].y, T);
-        p += 8u * n8;
-    }
-    crc = crc16_unswap(crc);
-    /* trailing bytes: the byte table is w1's [22,32) field table at byte << 2 (stream byte 7) */
-    while (p < b1) { crc = ((crc << 8) ^ crc16_unswap(T[CRC11_W1F2 + ((((crc >> 8) ^ bytes[p]) & 0xffu) << 2)])) & 0xffff; p++; }
-    return crc;
-}
 
 /* Fused-path cursor (4-slot ring).  ra is the LDS byte offset of ring word wi inside the
  * channel's ring: bits 2-3 word in block, 4-9 lane, 10-11 slot.  Moving it one word on is
@@ -3675,7 +3681,9 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     uint32_t nst = 0; /* vector-memory ops (PCM stores) issued by this wave since the last refill's DMAs */
     const bool sto = !(ablate & 2u);
     /* refill: wait for the previous refill's DMAs (every store since stays in flight), then
-     * issue the next blocks; stores issued after it are younger */
+     * issue the next blocks; stores issued after it are younger.  (Round 5: waiting for the
+     * refill before last instead, with the landing check covering the newest group, measured
+     * 32% slower on C2: a lane entering its newest group stalls the whole wave.) */
     auto refill = [&](bool want) {
         wait_vm_n(nst);
         z0.b.vendw = z0.b.iend * 4u;
@@ -3777,7 +3785,11 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
              * ds_write_b128), then lane l reads unit l & 7 of frame (l >> 3) + 8 i and stores
              * it: each store instruction writes 8 whole lines.  Every lane is active here
              * (a lane whose frame has ended stores nothing: its run address is 0). */
-            const uint64_t run = (valid && sto) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull;
+            uint64_t run = (valid && sto) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull;
+            /* timing ablation 0x10000000: the same stores into one 64 KB window per XCD (an
+             * L2-resident footprint: the HBM write traffic without the instructions); wrong PCM */
+            if ((ablate & 0x10000000u) && run)
+                run = (uint64_t)(uintptr_t)(out + (uint64_t)(blockIdx.x & 7u) * 65536u + lane * 1024u + ((n0 * 4u) & 1023u));
             const uint32_t rlo = (uint32_t)run, rhi = (uint32_t)(run >> 32);
             const uint32_t fr = lane & 31u, ul = lane & 7u;
 #pragma unroll
@@ -3831,7 +3843,13 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         if (br_pos(z1.b) > limit) ok = false;
         resume = br_pos(z1.b);
     }
-    /* CRC-16 of the frame bytes (read_frame_'s footer check @0x10011a01) */
+    /* CRC-16 of the frame bytes (read_frame_'s footer check @0x10011a01).  Round 5: the tail is
+     * 19% of this kernel on C2 (ablation 1), 7 points of it the re-read of the frame (ablation
+     * 0x40000000: the same work on L2-resident bytes).  A separate pass ahead of the decode
+     * (each frame over [offset, next offset), a wave per frame with 1 KB loads, the decode
+     * taking its verdict when the frame ends there) cost more than it saved: 2.2 ms against
+     * 1.7 ms at C2's 1,024 batches, 5 TB/s for the 11 GB, and no overlap with k_parse on a
+     * second stream. */
     uint32_t crc = crc_read;
     const bool need = ok && !(ablate & 1u);
     if (any_lane(need)) {
@@ -3839,7 +3857,13 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
         for (uint32_t i = lane; i < CRC11_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
         __syncthreads();
-        if (need) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
+        /* timing ablation 0x40000000: the same CRC work over a 1 MB window per XCD (L2-resident,
+         * each lane its own 16 KB: the re-read's HBM traffic without the work); result ignored */
+        const bool hotc = (ablate & 0x40000000u) != 0;
+        const uint8_t *cb = (const uint8_t *)words;
+        if (hotc) cb = cb + ((uint64_t)(blockIdx.x & 7u) * 64u + lane) * 16384u + (fi.frame_off & 63u) - fi.frame_off;
+        if (need) crc = st_crc16(cb, fi.frame_off, (hotc && end_byte - fi.frame_off > 16000u) ? fi.frame_off + 16000u : end_byte, T);
+        if (hotc) crc = crc_read;
     }
     if (ok && crc != crc_read) ok = false;
     if (ok) {
@@ -4910,7 +4934,9 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
                            out_sample_in, base_sample, info, pws, seg);
         return hipGetLastError();
     }
-    /* the parse order (walk length from the header bytes): a fixed-blocksize stream's frames
+    /* (Round 5: k_parse's occupancy is 5 waves per SIMD, LDS-bound; 4 or 3, by padding the LDS
+     * to 10 / 13 KB, measured the same on C2-C4.)
+     * the parse order (walk length from the header bytes): a fixed-blocksize stream's frames
      * all walk the same length (the last one aside), so the order only costs its three
      * launches there (C2: 0.12 ms per 1,024 batches) */
     const uint32_t *perm = nullptr;
