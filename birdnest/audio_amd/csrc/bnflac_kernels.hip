@@ -45,16 +45,39 @@
 __constant__ uint8_t g_crc8_tab[256];
 __constant__ uint16_t g_crc16_tab[8][256]; /* slice-by-8 */
 __constant__ uint16_t g_crc16_xpow[40];    /* x^(8*2^j) mod P for j < 40 */
-/* CRC-16 of an 8-byte block by six fields of 11/11/10 bits (crc16_step8le): the contribution
- * of each field value to the block's CRC (init 0).  The fields are bits [0,11), [11,22) and
- * [22,32) of the block's two words AS LOADED (little-endian: stream byte 0 in bits 0-7), so the
- * step needs no byte swap, and every entry is stored byte-swapped, so the running CRC stays in
- * that form and XORs straight into the first word's low 16 bits (round 5: the step is 18
- * add / shift-right / and / xor, all full-rate, instead of 21 with two v_perm and four v_bfe).
- * Table f at CRC11_OFF[f] entries: w0 fields 0-2, w1 fields 0-2.  20 KB. */
-#define CRC11_N 10240
-#define CRC11_W1F2 9216 /* w1 bits [22,32): stream byte 7 = index bits 2-9, i.e. the byte table at x << 2 */
-__constant__ uint16_t g_crc16_t11[CRC11_N];
+/* CRC-16 of an 8-byte block by fields of its two words (crc16_step8le): the contribution of
+ * each field value to the block's CRC (init 0).  The fields are bit ranges of the block's two
+ * words AS LOADED (little-endian: stream byte 0 in bits 0-7), so the step needs no byte swap,
+ * and every entry is stored byte-swapped, so the running CRC stays in that form and XORs
+ * straight into the first word's low 16 bits (round 5: shift-right / and / xor, all
+ * full-rate).  The field widths (CRC_LAYOUT) trade LDS bank conflicts for lookups: a table of
+ * 2,048 entries spreads a 32-lane group's random reads over 32 banks with several dwords
+ * each (~3.5-way on average), one of at most 64 entries (32 dwords) has one dword per bank,
+ * so its reads never conflict.
+ *   0: 11/11/10 bits per word, 6 lookups in 20 KB (the default);
+ *   1: 11/11/6/4 and 6/6/6/6/6/2, 10 lookups, two of them conflicted;
+ *   2: 6/6/6/6/6/2 per word, 12 conflict-free lookups in 1.8 KB.
+ * Round 5, same-box A/B: layout 2 is 2% slower on C2 (10.72 → 10.94 ms) and 1.6% on C3: the
+ * tail's extra address arithmetic costs more than the conflicts it removes.
+ * After the field tables of layouts 1 and 2: the byte table, for the trailing bytes. */
+#ifndef CRC_LAYOUT
+#define CRC_LAYOUT 0
+#endif
+#if CRC_LAYOUT == 0
+#define CRC_TAB_N 10240
+#define CRC_BYTE_OFF 9216 /* w1 bits [22,32): stream byte 7 = index bits 2-9 -- read at x << 2 */
+#define CRC_BYTE_SH 2
+#elif CRC_LAYOUT == 1
+#define CRC_TAB_N 4756
+#define CRC_BYTE_OFF 4500
+#define CRC_BYTE_SH 0
+#else
+#define CRC_TAB_N 904
+#define CRC_BYTE_OFF 648
+#define CRC_BYTE_SH 0
+#endif
+#define CRC11_N 10240 /* LDS the tail may use (the 20 KB of the rings and the flush tile) */
+__constant__ uint16_t g_crc16_t11[CRC_TAB_N];
 
 /* Debug event counters (wave-level events, enabled by ablate bit 0x100; timing runs
  * leave them off).  0 fused chunks, 1 generic chunks, 2 DMA landing waits, 3 slow Rice
@@ -1737,11 +1760,25 @@ DEV uint32_t crc16_step8(uint32_t crc, uint32_t w0, uint32_t w1, const lds_u16 *
 DEV uint32_t crc16_t11_at(const lds_u16 *T, uint32_t boff) {
     return *(const lds_u16 *)((const __attribute__((address_space(3))) uint8_t *)T + boff);
 }
+/* the six 6/6/6/6/6/2-bit fields of word x at table byte offset o (entries o/2 ..) */
+DEV uint32_t crc16_w6(const lds_u16 *T, uint32_t x, uint32_t o) {
+    return crc16_t11_at(T, o + ((x + x) & 0x7Eu)) ^ crc16_t11_at(T, o + 128u + ((x >> 5) & 0x7Eu)) ^
+           crc16_t11_at(T, o + 256u + ((x >> 11) & 0x7Eu)) ^ crc16_t11_at(T, o + 384u + ((x >> 17) & 0x7Eu)) ^
+           crc16_t11_at(T, o + 512u + ((x >> 23) & 0x7Eu)) ^ crc16_t11_at(T, o + 640u + ((x >> 29) & 0x6u));
+}
 DEV uint32_t crc16_step8le(uint32_t cs, uint32_t w0, uint32_t w1, const lds_u16 *T) {
     const uint32_t a = w0 ^ cs;
+#if CRC_LAYOUT == 0
     return crc16_t11_at(T, (a + a) & 0xFFEu) ^ crc16_t11_at(T, 4096u + ((a >> 10) & 0xFFEu)) ^
            crc16_t11_at(T, 8192u + ((a >> 21) & 0x7FEu)) ^ crc16_t11_at(T, 10240u + ((w1 + w1) & 0xFFEu)) ^
-           crc16_t11_at(T, 14336u + ((w1 >> 10) & 0xFFEu)) ^ crc16_t11_at(T, 2u * CRC11_W1F2 + ((w1 >> 21) & 0x7FEu));
+           crc16_t11_at(T, 14336u + ((w1 >> 10) & 0xFFEu)) ^ crc16_t11_at(T, 18432u + ((w1 >> 21) & 0x7FEu));
+#elif CRC_LAYOUT == 1
+    return crc16_t11_at(T, (a + a) & 0xFFEu) ^ crc16_t11_at(T, 4096u + ((a >> 10) & 0xFFEu)) ^
+           crc16_t11_at(T, 8192u + ((a >> 21) & 0x7Eu)) ^ crc16_t11_at(T, 8320u + ((a >> 27) & 0x1Eu)) ^
+           crc16_w6(T, w1, 8352u);
+#else
+    return crc16_w6(T, a, 0u) ^ crc16_w6(T, w1, 648u);
+#endif
 }
 DEV uint32_t crc16_unswap(uint32_t cs) { return ((cs >> 8) | (cs << 8)) & 0xffffu; }
 DEV uint32_t crc16_range(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
@@ -1846,7 +1883,7 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
     }
     crc = crc16_unswap(crc);
     /* trailing bytes: the byte table is w1's [22,32) field table at byte << 2 (stream byte 7) */
-    while (p < b1) { crc = ((crc << 8) ^ crc16_unswap(T[CRC11_W1F2 + ((((crc >> 8) ^ bytes[p]) & 0xffu) << 2)])) & 0xffff; p++; }
+    while (p < b1) { crc = ((crc << 8) ^ crc16_unswap(T[CRC_BYTE_OFF + ((((crc >> 8) ^ bytes[p]) & 0xffu) << CRC_BYTE_SH)])) & 0xffff; p++; }
     return crc;
 }
 
@@ -3855,7 +3892,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     if (any_lane(need)) {
         wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
         lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
-        for (uint32_t i = lane; i < CRC11_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
+        for (uint32_t i = lane; i < CRC_TAB_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
         __syncthreads();
         /* timing ablation 0x40000000: the same CRC work over a 1 MB window per XCD (L2-resident,
          * each lane its own 16 KB: the re-read's HBM traffic without the work); result ignored */
@@ -4422,7 +4459,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     if (any_lane(need)) {
         wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
         lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
-        for (uint32_t i = lane; i < CRC11_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
+        for (uint32_t i = lane; i < CRC_TAB_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
         __syncthreads();
         if (need) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
     }
@@ -4462,10 +4499,19 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
     { /* field tables (crc16_step8le) from the byte table (crc16x8[0]): the CRC of the 8-byte
        * block holding v in bits [lo, lo + wd) of word j as loaded (LE bit p of word j = stream
        * byte 4j + p / 8, bit p % 8 of that byte), stored byte-swapped */
-        static const uint32_t lo[6] = {0, 11, 22, 0, 11, 22}, wd[6] = {11, 11, 10, 11, 11, 10}, wj[6] = {0, 0, 0, 1, 1, 1};
-        uint16_t t11[CRC11_N];
+#if CRC_LAYOUT == 0
+        static const uint32_t lo[] = {0, 11, 22, 0, 11, 22}, wd[] = {11, 11, 10, 11, 11, 10}, wj[] = {0, 0, 0, 1, 1, 1};
+#elif CRC_LAYOUT == 1
+        static const uint32_t lo[] = {0, 11, 22, 28, 0, 6, 12, 18, 24, 30}, wd[] = {11, 11, 6, 4, 6, 6, 6, 6, 6, 2},
+                              wj[] = {0, 0, 0, 0, 1, 1, 1, 1, 1, 1};
+#else
+        static const uint32_t lo[] = {0, 6, 12, 18, 24, 30, 0, 6, 12, 18, 24, 30}, wd[] = {6, 6, 6, 6, 6, 2, 6, 6, 6, 6, 6, 2},
+                              wj[] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1};
+#endif
+        constexpr int NF = (int)(sizeof lo / sizeof lo[0]);
+        uint16_t t11[CRC_TAB_N];
         uint32_t at = 0;
-        for (int fld = 0; fld < 6; fld++)
+        for (int fld = 0; fld < NF; fld++)
             for (uint32_t v = 0; v < (1u << wd[fld]); v++) {
                 uint8_t blk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
                 for (uint32_t i = 0; i < wd[fld]; i++)
@@ -4477,6 +4523,9 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
                 for (int by = 0; by < 8; by++) c = ((c << 8) ^ crc16x8[((c >> 8) ^ blk[by]) & 0xffu]) & 0xffffu;
                 t11[at++] = (uint16_t)(((c >> 8) | (c << 8)) & 0xffffu);
             }
+        if (CRC_LAYOUT != 0) /* the byte table, byte-swapped like the fields */
+            for (uint32_t x = 0; x < 256u; x++) t11[at++] = (uint16_t)(((crc16x8[x] >> 8) | (crc16x8[x] << 8)) & 0xffffu);
+        if (at != CRC_TAB_N) return hipErrorInvalidValue;
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_t11), t11, sizeof t11);
         if (e != hipSuccess) return e;
     }
