@@ -459,6 +459,7 @@ void bnsyn_default_params(bnsyn_params *p) {
     p->stereo_mode = BNSYN_STEREO_INDEPENDENT;
     p->level = 0.5;
     p->noise = 0.006;
+    p->impulse_permille = 0;
     p->seed = 1;
     p->write_header = 1;
     p->force_sr_code = -1;
@@ -549,6 +550,8 @@ int bnsyn_encode(const bnsyn_params *p, uint8_t *out, size_t cap, size_t *out_le
         double nstd = p->noise * fs;
         for (uint64_t i = 0; i < total * C; i++) {
             double v = raw[i] * scale + nstd * rng_gauss(&rng);
+            if (p->impulse_permille > 0 && (int)rng_below(&rng, 1000) < p->impulse_permille)
+                v += (rng_below(&rng, 2) ? 0.4 : -0.4) * fs;
             int64_t q = (int64_t)llround(v);
             if (q > smax) q = smax;
             if (q < smin) q = smin;

@@ -61,6 +61,9 @@ typedef struct {
     int32_t odd_headers;        /* 1: use 8/16-bit explicit blocksize and explicit-rate codes */
     int32_t prec_clamp;         /* 1: clamp LPC precision like libFLAC's encoder (<= 17-bit subframes
                                  * stay on the 32-bit restore path); 0: any precision (64-bit path) */
+    int32_t impulse_permille;   /* probability per sample of an impulse of 0.4 x full scale: residuals far
+                                 * above the partition's Rice parameter (unary prefixes beyond a
+                                 * 32-bit window); 0 leaves the signal (and its random stream) as before */
 } bnsyn_params;
 
 void bnsyn_default_params(bnsyn_params *p);

@@ -30,7 +30,7 @@ class _Params(ctypes.Structure):
         ("noise", ctypes.c_double), ("seed", ctypes.c_uint64), ("rice2", ctypes.c_int32),
         ("escape_permille", ctypes.c_int32), ("write_header", ctypes.c_int32),
         ("force_sr_code", ctypes.c_int32), ("odd_headers", ctypes.c_int32),
-        ("prec_clamp", ctypes.c_int32),
+        ("prec_clamp", ctypes.c_int32), ("impulse_permille", ctypes.c_int32),
     ]
 
 
@@ -60,6 +60,7 @@ class SynthParams:
     force_sr_code: int = -1
     odd_headers: int = 0
     prec_clamp: int = 0   # 1: libFLAC encoder's precision clamp (see bnflac_synth.c)
+    impulse_permille: int = 0  # impulses of 0.4 x full scale per 1000 samples (long Rice prefixes)
 
 
 @dataclasses.dataclass

@@ -529,6 +529,41 @@ def test_stereo_fast_path_layouts(gpu, fmt_name, cfg, kw, decode_mode):
     assert np.array_equal(s.pcm, oracle.interleave(ev, opcm))
 
 
+@pytest.mark.parametrize("fmt_name", ["OUT_FLACDECODER", "OUT_INTERLEAVED32"])
+@LANE
+def test_long_rice_prefixes_small_parameters(gpu, fmt_name, decode_mode):
+    """Impulses in a C2-shaped stream (Rice parameters ~8, so k_parse takes its bulk instance):
+    unary prefixes of ~100 bits, far beyond a 32-bit window, where a pair of codewords does
+    not fit -- k_parse's bulk steps hand the lane to the generic reader, k_decode_st's fused
+    pairs take st_rare_pair.  Bit-exact against the source and the oracle, every frame kept by
+    k_decode_st, and its slow-codeword counter (ablation 0x100's stats) nonzero."""
+    import ctypes
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, dec = gpu
+    fmt = getattr(libflac, fmt_name)
+    p = synth.config("C2", nframes=70, last_blocksize=0, impulse_permille=2)
+    s = synth.encode(p)
+    data = s.data.tobytes()
+    buf = (ctypes.c_uint64 * 16)()
+    dec.L.bnflac_debug_stats(buf, 1)
+    dec.L.bnflac_debug_set_ablate(0x100)
+    try:
+        out, info, sp = _decode_batch(gpu, data, s.frame_offsets, fmt)
+    finally:
+        dec.L.bnflac_debug_set_ablate(0)
+    dec.L.bnflac_debug_stats(buf, 1)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    assert (info["flags"] & FL_ST).all() and not (info["flags"] & FL_REDO).any(), info["flags"]
+    assert buf[3] > 0, list(buf)
+    if fmt == libflac.OUT_INTERLEAVED32:
+        assert np.array_equal(out.view("<i4").reshape(-1, 2), s.pcm)
+    else:
+        assert out.tobytes() == (s.pcm.astype(np.int64) & 0xFFFF).astype("<u2").tobytes()
+    ev, opcm = oracle.run(data)
+    assert np.array_equal(s.pcm, oracle.interleave(ev, opcm))
+
+
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C4"])
 @LANE
 def test_stereo_handback_matches(gpu, cfg, decode_mode):

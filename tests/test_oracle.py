@@ -108,6 +108,16 @@ def test_config_roundtrip(cfg):
     assert np.array_equal(oracle.interleave(ev, pcm), s.pcm)
 
 
+def test_long_rice_prefixes_roundtrip():
+    """Impulses (generator impulse_permille): residuals whose unary prefixes run ~100 bits in
+    partitions coded with small Rice parameters; the oracle's unary reader returns the source."""
+    s = synth.encode(synth.config("C2", nframes=4, last_blocksize=0, impulse_permille=3))
+    ev, pcm = oracle.run(s.data.tobytes())
+    assert np.array_equal(oracle.interleave(ev, pcm), s.pcm)
+    plain = synth.encode(synth.config("C2", nframes=4, last_blocksize=0))
+    assert len(s.data) > len(plain.data)  # the impulses cost bits: they are in the stream
+
+
 def test_flacdecoder_pack_rules():
     # FLACDecoder.cs:543-562 stereo: [L lo, L hi, R lo, R hi]
     s = synth.encode(synth.config("C2", nframes=3))

@@ -29,7 +29,7 @@ def draw(rng):
               rice2=int(rng.integers(0, 2)), escape_permille=int(rng.choice([0, 0, 30])),
               wasted_bits_max=int(rng.choice([0, 0, 2, 5])), level=float(rng.uniform(0.02, 0.95)),
               noise=float(rng.choice([0.0003, 0.004, 0.03, 0.3])), seed=int(rng.integers(1, 1 << 30)),
-              prec_clamp=int(rng.integers(0, 2)), variable_blocksize=var,
+              prec_clamp=int(rng.integers(0, 2)), variable_blocksize=var, impulse_permille=int(rng.choice([0, 0, 0, 2])),
               sample_rate=int(rng.choice([8000, 44100, 48000, 96000, 192000])))
     if mode == synth.SUB_FIXED:
         kw["order"] = int(rng.integers(0, 5))
