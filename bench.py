@@ -884,10 +884,13 @@ def main():
         # decoding its own, then the gather of every rank's PCM to rank 0 over RCCL
         del wl
         torch.cuda.empty_cache()
-        r = c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank)
-        line["legs"] = {"C5_flow": c5_summary(r, args, world)}
-        line["legs"]["C5_flow"]["config"] = {"workload": CONFIGS["C5"]["desc"], "files": r["files"],
-                                             "parallelism": f"files sharded per rank x{world} + RCCL gather to rank 0"}
+        try:  # the headline above is measured: an error in the side flow must not lose its line
+            r = c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank)
+            line["legs"] = {"C5_flow": c5_summary(r, args, world)}
+            line["legs"]["C5_flow"]["config"] = {"workload": CONFIGS["C5"]["desc"], "files": r["files"],
+                                                 "parallelism": f"files sharded per rank x{world} + RCCL gather to rank 0"}
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line, never swallowed
+            line["legs"] = {"C5_flow": {"error": f"{type(e).__name__}: {e}"[:500]}}
     if rank == 0:
         js = json.dumps(line)
         print(js, flush=True)
