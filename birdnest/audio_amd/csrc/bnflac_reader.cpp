@@ -361,7 +361,15 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
     r->stride = bnflac_out_stride(out_format, &r->sp);
     r->nbytes = nbytes;
     const size_t padded = (size_t)((nbytes + 15) & ~15ull) + 16;
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(nbytes / 8 + 16, 1u << 30); /* a frame is >= 9 bytes */
+    /* Frame records.  A frame is >= 9 bytes, so nbytes / 8 bounds the chain, but at 128 B a
+     * record that bound is 16x the stream (171 MB for a 10.7 MB C2 stream): past the pool cap,
+     * so every open allocated it and every close paid a 0.2 ms hipFree.  STREAMINFO's total
+     * and minimum blocksize give the usual count (frames past the total are dropped by the
+     * index); a chain longer than that re-indexes at the full bound below. */
+    const uint32_t cap_full = (uint32_t)std::min<uint64_t>(nbytes / 8 + 16, 1u << 30);
+    uint32_t cap = cap_full;
+    if (r->sp.total_samples && r->sp.min_blocksize >= 16)
+        cap = (uint32_t)std::min<uint64_t>(cap_full, r->sp.total_samples / r->sp.min_blocksize + 16);
     size_t cap_n = 16;
     if ((!r->stream && hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) ||
         !dgrow(r->d_bytes, r->cap_bytes, padded) || !dgrow(r->d_offs, r->cap_offs, 8ull * cap) ||
@@ -380,17 +388,28 @@ BNFLAC_API int bnflac_reader_open(int device, const uint8_t *bytes, uint64_t nby
         return rfail("bnflac_reader_open: H2D copy failed");
     }
     tr.mark("h2d", r->stream);
-    if (bnflac_index_stream(r->ctx, (const uint8_t *)r->d_bytes, nbytes, first, &r->sp, (uint64_t *)r->d_offs,
-                            (uint64_t *)r->d_os, (bnflac_frame_info *)r->d_info, cap, (uint32_t *)r->d_n, r->stream)) {
-        const std::string e = bnflac_last_error();
-        release(r, false);
-        return rfail("bnflac_reader_open: " + e);
-    }
     uint32_t nf = 0;
-    if (hipMemcpyAsync(&nf, r->d_n, 4, hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
-        hipStreamSynchronize(r->stream) != hipSuccess || nf > cap) {
-        release(r, false);
-        return rfail("bnflac_reader_open: frame index failed");
+    for (;;) {
+        if (bnflac_index_stream(r->ctx, (const uint8_t *)r->d_bytes, nbytes, first, &r->sp, (uint64_t *)r->d_offs,
+                                (uint64_t *)r->d_os, (bnflac_frame_info *)r->d_info, cap, (uint32_t *)r->d_n,
+                                r->stream)) {
+            const std::string e = bnflac_last_error();
+            release(r, false);
+            return rfail("bnflac_reader_open: " + e);
+        }
+        if (hipMemcpyAsync(&nf, r->d_n, 4, hipMemcpyDeviceToHost, r->stream) != hipSuccess ||
+            hipStreamSynchronize(r->stream) != hipSuccess || (nf > cap && cap == cap_full)) {
+            release(r, false);
+            return rfail("bnflac_reader_open: frame index failed");
+        }
+        if (nf <= cap) break;
+        /* more frames than STREAMINFO implies: index again with room for any chain */
+        cap = cap_full;
+        if (!dgrow(r->d_offs, r->cap_offs, 8ull * cap) || !dgrow(r->d_os, r->cap_os, 8ull * cap) ||
+            !dgrow(r->d_info, r->cap_info, sizeof(bnflac_frame_info) * cap)) {
+            release(r, false);
+            return rfail("bnflac_reader_open: out of device memory");
+        }
     }
     tr.mark("index", r->stream);
     r->nframes = nf;

@@ -722,6 +722,27 @@ def test_reader_c2_windows_and_chunks(gpu, window, chunk):
         r.close()
 
 
+def test_reader_more_frames_than_streaminfo_implies(gpu):
+    """The reader sizes its frame records from STREAMINFO (total / minimum blocksize + 16).  A
+    variable-blocksize stream whose STREAMINFO claims a larger minimum than its frames use
+    overflows that guess: open re-indexes at the byte bound and still reads every frame."""
+    from birdnest.audio_amd import synth
+    torch, libflac, _ = gpu
+    s = synth.encode(synth.config("C4", nframes=300))
+    d = bytearray(s.data.tobytes())
+    assert d[:4] == b"fLaC" and (d[4] & 0x7F) == 0  # STREAMINFO first: min/max blocksize at 8..11
+    assert d[int(s.frame_offsets[0]) + 1] & 1  # variable-blocksize frames (sample-numbered)
+    d[8:12] = (16384).to_bytes(2, "big") + (65535).to_bytes(2, "big")
+    assert s.pcm.shape[0] // 16384 + 16 < 300  # the guess is short: the retry runs
+    for win in (256, 7):
+        r = libflac.Reader(bytes(d), libflac.OUT_FLACDECODER, window_frames=win)
+        try:
+            assert r.nframes == 300
+            assert r.read_all(16384) == s.pcm.astype("<i2").tobytes()
+        finally:
+            r.close()
+
+
 def test_reader_refuses_damaged_stream(gpu):
     torch, libflac, _ = gpu
     data = _read("err_crc16_mismatch")
