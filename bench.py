@@ -23,7 +23,8 @@ them, then the interleaved PCM gathered to rank 0 over RCCL (shard.gather_bytes,
 point-to-point receives); decode-only and decode+gather times are reported separately.
 
 value        = decoded samples (blocksize x channels) per second, whole
-               job over all ranks (weak scaling for C2-C4: every rank decodes its own batches).
+               job over all ranks (weak scaling for C2-C4: a corpus of N x B batches, rank r decoding
+               its contiguous B of them, a stream of its own).
 roofline     = the dominant launch (the decode launch): algorithmic bytes (compressed frame bytes +
                PCM bytes written) / its HIP-event-timed average duration on the stream it
                runs on, vs 8 TB/s HBM; step_frac = the same bytes / the whole step (k_parse included).
@@ -99,6 +100,10 @@ def parse_args():
     ap.add_argument("--nccl-timeout", type=int, default=180, help="seconds before a stuck collective aborts the run")
     ap.add_argument("--no-c5-flow", action="store_true",
                     help="N > 1: skip the C5 shard -> index -> decode -> RCCL gather leg")
+    ap.add_argument("--c5-split", type=int, default=1,
+                    help="C5 flow at N > 1: the in-step gather's groups are K frame ranges of each file "
+                         "(default 1: whole files; one file's decode is latency-bound, so K pieces decode "
+                         "in about K times its time)")
     ap.add_argument("--c5-batch", action="store_true",
                     help="--config C5 as one batch of the 8 files' frames (the C5 leg's workload; --stats/--ablate apply)")
     ap.add_argument("--stats", action="store_true", help="report k_decode event counters (one extra step)")
@@ -570,43 +575,57 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank, files=None,
     warmup = args.warmup if warmup is None else warmup
     p0 = synth.config("C5")
     ranges = shard.partition([p0.nframes * p0.blocksize] * F, world)  # equal files: F/world each
-    lo, hi = ranges[rank]
-    mine = list(range(lo, hi))
-    streams = [synth.encode(synth.config("C5", seed=5 + 1000 * i)) for i in mine]
-    sp = libflac.StreamParams.from_synth(p0, streams[0].nsamples if streams else 0)
-    fmt = libflac.OUT_FILEREADER
-    stride = libflac.out_stride(fmt, sp)
-    lens = [(len(s.data) + 255) // 256 * 256 for s in streams]
-    base = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) if streams else np.zeros(1, np.int64)
-    d_bytes = torch.zeros(int(base[-1]) + 64, dtype=torch.uint8, device=dev)
-    offs, osmp, nsmp = [], [], 0
-    for i, s in enumerate(streams):
-        n = len(s.data)
-        d_bytes[int(base[i]):int(base[i]) + n] = torch.from_numpy(s.data.copy()).to(dev)
-        o, os_, _, nf = dec.index_stream(d_bytes[int(base[i]):], n, int(s.frame_offsets[0]), sp, len(s.frame_offsets) + 8)
-        assert nf == len(s.frame_offsets), "GPU frame index disagrees with the generator"
-        offs.append(o[:nf].cpu().numpy() + int(base[i]))
-        osmp.append(os_[:nf].cpu().numpy() + nsmp)
-        nsmp += s.nsamples
-    nframes = int(sum(len(o) for o in offs))
-    d_offs = torch.from_numpy(np.concatenate(offs) if offs else np.zeros(0, np.int64)).to(dev)
-    d_os = torch.from_numpy(np.concatenate(osmp) if osmp else np.zeros(0, np.int64)).to(dev)
-    d_out = torch.empty(max(nsmp * stride, 1), dtype=torch.uint8, device=dev)
-    d_out2 = torch.empty_like(d_out)  # the overlapped flow's second output buffer
-    d_info = torch.zeros(max(nframes, 1) * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    nb = int(base[-1])
+    # The rank-local setup (generate, index, warm up) fails, if at all, on one rank alone: every
+    # rank then learns it at one all_reduce that all of them reach, and all raise together, so
+    # no rank is left waiting in a later collective (main() reports the error in the C5 leg).
+    err = None
+    try:
+        lo, hi = ranges[rank]
+        mine = list(range(lo, hi))
+        streams = [synth.encode(synth.config("C5", seed=5 + 1000 * i)) for i in mine]
+        sp = libflac.StreamParams.from_synth(p0, streams[0].nsamples if streams else 0)
+        fmt = libflac.OUT_FILEREADER
+        stride = libflac.out_stride(fmt, sp)
+        lens = [(len(s.data) + 255) // 256 * 256 for s in streams]
+        base = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) if streams else np.zeros(1, np.int64)
+        d_bytes = torch.zeros(int(base[-1]) + 64, dtype=torch.uint8, device=dev)
+        offs, osmp, nsmp = [], [], 0
+        for i, s in enumerate(streams):
+            n = len(s.data)
+            d_bytes[int(base[i]):int(base[i]) + n] = torch.from_numpy(s.data.copy()).to(dev)
+            o, os_, _, nf = dec.index_stream(d_bytes[int(base[i]):], n, int(s.frame_offsets[0]), sp, len(s.frame_offsets) + 8)
+            assert nf == len(s.frame_offsets), "GPU frame index disagrees with the generator"
+            offs.append(o[:nf].cpu().numpy() + int(base[i]))
+            osmp.append(os_[:nf].cpu().numpy() + nsmp)
+            nsmp += s.nsamples
+        nframes = int(sum(len(o) for o in offs))
+        d_offs = torch.from_numpy(np.concatenate(offs) if offs else np.zeros(0, np.int64)).to(dev)
+        d_os = torch.from_numpy(np.concatenate(osmp) if osmp else np.zeros(0, np.int64)).to(dev)
+        d_out = torch.empty(max(nsmp * stride, 1), dtype=torch.uint8, device=dev)
+        d_out2 = torch.empty_like(d_out)  # the overlapped flow's second output buffer
+        d_info = torch.zeros(max(nframes, 1) * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        nb = int(base[-1])
 
-    def decode(out=d_out, e=None):
-        if nframes:
-            dec.parse_frames(d_bytes, nb, d_offs, nframes, sp, d_info, d_out_sample=d_os, stream=stream)
-            if e is not None:
-                e[1].record(stream)
-            dec.decode_parsed(d_bytes, nb, nframes, sp, fmt, out, d_info, stream=stream)
+        def decode(out=d_out, e=None):
+            if nframes:
+                dec.parse_frames(d_bytes, nb, d_offs, nframes, sp, d_info, d_out_sample=d_os, stream=stream)
+                if e is not None:
+                    e[1].record(stream)
+                dec.decode_parsed(d_bytes, nb, nframes, sp, fmt, out, d_info, stream=stream)
 
-    for _ in range(warmup):
-        decode()
-    torch.cuda.synchronize(dev)
+        for _ in range(warmup):
+            decode()
+        torch.cuda.synchronize(dev)
+    except Exception as e:  # noqa: BLE001 -- re-raised below on every rank
+        err = f"rank {rank}: {type(e).__name__}: {e}"
+    if world > 1:
+        flag = torch.tensor([0 if err else 1], device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()):
+            raise RuntimeError(err or "C5 setup failed on another rank")
+    elif err:
+        raise RuntimeError(err)
     if world > 1:
         dist.barrier()
     ev = []
@@ -671,18 +690,21 @@ def c5_job(args, torch, dist, dev, libflac, synth, dec, world, rank, files=None,
     # its decode is enqueued, so group g's transfer runs beside group g + 1's decode
     t_grp, gathered_grp = t_all, None
     if world > 1:
-        fb = [0] + list(np.cumsum([len(o) for o in offs]))          # frame range of each file
-        sb = [0] + list(np.cumsum([s.nsamples * stride for s in streams]))  # its byte range in d_out
-        gsz = shard.gather_group_sizes([int(sb[i + 1] - sb[i]) for i in range(len(streams))], device=dev)
+        # groups: the rank's files, or (--c5-split K) K frame ranges of each file; a group's
+        # bytes run from its first frame's output sample to the next group's
+        franges, _ = shard.frame_groups([len(o) for o in offs], getattr(args, "c5_split", 1))
+        fstart = np.concatenate(osmp + [np.array([nsmp], np.int64)]) if osmp else np.zeros(1, np.int64)
+        gb = [(int(fstart[a]) * stride, int(fstart[b]) * stride) for a, b in franges]
+        gsz = shard.gather_group_sizes([b - a for a, b in gb], device=dev)
 
         def grouped():
             gg = shard.GroupGather(gsz, d_out)
-            for i in range(len(streams)):
-                f0, f1 = int(fb[i]), int(fb[i + 1])
-                di = d_info[f0 * libflac.FRAME_INFO_BYTES:f1 * libflac.FRAME_INFO_BYTES]
-                dec.parse_frames(d_bytes, nb, d_offs[f0:f1], f1 - f0, sp, di, d_out_sample=d_os[f0:f1], stream=stream)
-                dec.decode_parsed(d_bytes, nb, f1 - f0, sp, fmt, d_out, di, stream=stream)
-                gg.post(i, d_out[int(sb[i]):int(sb[i + 1])])
+            for g, (f0, f1) in enumerate(franges):
+                if f1 > f0:
+                    di = d_info[f0 * libflac.FRAME_INFO_BYTES:f1 * libflac.FRAME_INFO_BYTES]
+                    dec.parse_frames(d_bytes, nb, d_offs[f0:f1], f1 - f0, sp, di, d_out_sample=d_os[f0:f1], stream=stream)
+                    dec.decode_parsed(d_bytes, nb, f1 - f0, sp, fmt, d_out, di, stream=stream)
+                gg.post(g, d_out[gb[g][0]:gb[g][1]])
             return gg.wait()
 
         grouped()
@@ -804,8 +826,14 @@ def main():
             dist.destroy_process_group()
         return
 
+    # The job's corpus: world x B batches, cut into contiguous ranges by shard.partition (equal
+    # batches: B per rank, weak scaling); rank r's batches hold its own stream (seed + 7919 r,
+    # rank 0 the config's stream), so no two ranks decode the same bytes.
+    from birdnest.audio_amd import shard
     B = args.batches or c["batches"]
-    wl = Workload(cfg, B, args.frames, torch, dev, libflac, synth, dec, seed=2 if cfg == "C2" else None)
+    b0, b1 = shard.partition([1] * (world * B), world)[rank]
+    seed0 = 2 if cfg == "C2" else synth.config(cfg).seed
+    wl = Workload(cfg, b1 - b0, args.frames, torch, dev, libflac, synth, dec, seed=seed0 + 7919 * rank)
     elapsed, t_parse, t_decode = timed(wl, args.steps, args.warmup, stream, world, dist, dev)
     ok = wl.check()
     if world > 1:
@@ -813,7 +841,12 @@ def main():
         dist.all_reduce(o, op=dist.ReduceOp.MIN)
         ok = bool(o.item())
     step_ms = elapsed / args.steps * 1e3
-    value = wl.samples * args.steps * world / elapsed / 1e6
+    samples = wl.samples
+    if world > 1:  # every rank's own count (its stream's samples)
+        t = torch.tensor([samples], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        samples = int(t.item())
+    value = samples * args.steps / elapsed / 1e6
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -829,7 +862,7 @@ def main():
         "data": f"synthetic: deterministic generator, BASELINE {cfg} frame shape",
         "config": {"workload": c["desc"], "frames_per_batch": wl.nf1, "batches_per_step": B,
                    "compressed_bytes_per_batch": wl.fb_in, "pcm_bytes_per_batch": wl.pcm1,
-                   "parallelism": f"frames sharded per rank x{world}"},
+                   "parallelism": f"corpus of {world} x {B} batches partitioned per rank (shard.partition) x{world}"},
         "per_gpu_value": round(value / world, 2),
         "bitexact": ok,
         "roofline": roofline(wl.alg_bytes, t_decode, t_parse, step_ms, measured_traffic(cfg, B, wl.nf1)),

@@ -45,40 +45,6 @@
 __constant__ uint8_t g_crc8_tab[256];
 __constant__ uint16_t g_crc16_tab[8][256]; /* slice-by-8 */
 __constant__ uint16_t g_crc16_xpow[40];    /* x^(8*2^j) mod P for j < 40 */
-/* CRC-16 of an 8-byte block by fields of its two words (crc16_step8le): the contribution of
- * each field value to the block's CRC (init 0).  The fields are bit ranges of the block's two
- * words AS LOADED (little-endian: stream byte 0 in bits 0-7), so the step needs no byte swap,
- * and every entry is stored byte-swapped, so the running CRC stays in that form and XORs
- * straight into the first word's low 16 bits (round 5: shift-right / and / xor, all
- * full-rate).  The field widths (CRC_LAYOUT) trade LDS bank conflicts for lookups: a table of
- * 2,048 entries spreads a 32-lane group's random reads over 32 banks with several dwords
- * each (~3.5-way on average), one of at most 64 entries (32 dwords) has one dword per bank,
- * so its reads never conflict.
- *   0: 11/11/10 bits per word, 6 lookups in 20 KB (the default);
- *   1: 11/11/6/4 and 6/6/6/6/6/2, 10 lookups, two of them conflicted;
- *   2: 6/6/6/6/6/2 per word, 12 conflict-free lookups in 1.8 KB.
- * Round 5, same-box A/B: layout 2 is 2% slower on C2 (10.72 → 10.94 ms) and 1.6% on C3: the
- * tail's extra address arithmetic costs more than the conflicts it removes.
- * After the field tables of layouts 1 and 2: the byte table, for the trailing bytes. */
-#ifndef CRC_LAYOUT
-#define CRC_LAYOUT 0
-#endif
-#if CRC_LAYOUT == 0
-#define CRC_TAB_N 10240
-#define CRC_BYTE_OFF 9216 /* w1 bits [22,32): stream byte 7 = index bits 2-9 -- read at x << 2 */
-#define CRC_BYTE_SH 2
-#elif CRC_LAYOUT == 1
-#define CRC_TAB_N 4756
-#define CRC_BYTE_OFF 4500
-#define CRC_BYTE_SH 0
-#else
-#define CRC_TAB_N 904
-#define CRC_BYTE_OFF 648
-#define CRC_BYTE_SH 0
-#endif
-#define CRC11_N 10240 /* LDS the tail may use (the 20 KB of the rings and the flush tile) */
-__constant__ uint16_t g_crc16_t11[CRC_TAB_N];
-
 /* Debug event counters (wave-level events, enabled by ablate bit 0x100; timing runs
  * leave them off).  0 fused chunks, 1 generic chunks, 2 DMA landing waits, 3 slow Rice
  * codewords, 4 refills, 5 waves. */
@@ -242,6 +208,7 @@ DEV void dma_block(const BR &b, uint32_t j, uint32_t slot) { /* one 16-byte bloc
  * row still receives lane l's 16 bytes at +16 l. */
 template <int OFF>
 DEV void lds_dma16_off(const void *g, lds_u32 *row) {
+    dma_check_base(row); /* the row the data lands in (the base passed is row - OFF / 4) */
     __builtin_amdgcn_global_load_lds((gvoid *)g, (lds_void *)(row - OFF / 4), 16, OFF, 0);
 }
 
@@ -1465,7 +1432,8 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 }
 
 /* ==================================================================== k_parse */
-#define PARSE_RD 8 /* ring slots per lane (8 KB of LDS per wave, 5 waves per SIMD); 4 slots: 8 waves but 3% slower */
+#define PARSE_RD 8 /* ring slots per lane (8 KB of LDS per wave, 5 waves per SIMD) */
+static_assert(PARSE_RD == 8, "pk_ra and the walk's pair steps (slot masks 0x3F3 / 0x1C0C, slot bits 10-12) assume an 8-slot ring");
 /* One lane per candidate frame: header + cursor walk over subframes 0..C-2.  Also
  * flags frames with an LPC order above 8 (they go to k_decode<32>). */
 DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const uint64_t *__restrict__ frame_offs,
@@ -1753,34 +1721,6 @@ DEV uint32_t crc16_step8(uint32_t crc, uint32_t w0, uint32_t w1, const lds_u16 *
            T[4 * 256 + (a & 0xff)] ^ T[3 * 256 + (w1 >> 24)] ^ T[2 * 256 + ((w1 >> 16) & 0xff)] ^
            T[1 * 256 + ((w1 >> 8) & 0xff)] ^ T[w1 & 0xff];
 }
-/* the same 8-byte step with 6 lookups instead of 8 (tables: g_crc16_t11 in LDS).  cs: the CRC
- * so far, byte-swapped (its high byte in bits 0-7); w0, w1: the block's two words as loaded.
- * The table offsets are byte offsets of field * 2, so each lookup address is one shift-right
- * (or add) and one and. */
-DEV uint32_t crc16_t11_at(const lds_u16 *T, uint32_t boff) {
-    return *(const lds_u16 *)((const __attribute__((address_space(3))) uint8_t *)T + boff);
-}
-/* the six 6/6/6/6/6/2-bit fields of word x at table byte offset o (entries o/2 ..) */
-DEV uint32_t crc16_w6(const lds_u16 *T, uint32_t x, uint32_t o) {
-    return crc16_t11_at(T, o + ((x + x) & 0x7Eu)) ^ crc16_t11_at(T, o + 128u + ((x >> 5) & 0x7Eu)) ^
-           crc16_t11_at(T, o + 256u + ((x >> 11) & 0x7Eu)) ^ crc16_t11_at(T, o + 384u + ((x >> 17) & 0x7Eu)) ^
-           crc16_t11_at(T, o + 512u + ((x >> 23) & 0x7Eu)) ^ crc16_t11_at(T, o + 640u + ((x >> 29) & 0x6u));
-}
-DEV uint32_t crc16_step8le(uint32_t cs, uint32_t w0, uint32_t w1, const lds_u16 *T) {
-    const uint32_t a = w0 ^ cs;
-#if CRC_LAYOUT == 0
-    return crc16_t11_at(T, (a + a) & 0xFFEu) ^ crc16_t11_at(T, 4096u + ((a >> 10) & 0xFFEu)) ^
-           crc16_t11_at(T, 8192u + ((a >> 21) & 0x7FEu)) ^ crc16_t11_at(T, 10240u + ((w1 + w1) & 0xFFEu)) ^
-           crc16_t11_at(T, 14336u + ((w1 >> 10) & 0xFFEu)) ^ crc16_t11_at(T, 18432u + ((w1 >> 21) & 0x7FEu));
-#elif CRC_LAYOUT == 1
-    return crc16_t11_at(T, (a + a) & 0xFFEu) ^ crc16_t11_at(T, 4096u + ((a >> 10) & 0xFFEu)) ^
-           crc16_t11_at(T, 8192u + ((a >> 21) & 0x7Eu)) ^ crc16_t11_at(T, 8320u + ((a >> 27) & 0x1Eu)) ^
-           crc16_w6(T, w1, 8352u);
-#else
-    return crc16_w6(T, a, 0u) ^ crc16_w6(T, w1, 648u);
-#endif
-}
-DEV uint32_t crc16_unswap(uint32_t cs) { return ((cs >> 8) | (cs << 8)) & 0xffffu; }
 DEV uint32_t crc16_range(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
     uint32_t crc = 0;
     uint64_t p = b0;
@@ -1824,23 +1764,77 @@ DEV uint32_t crc16_shift(uint32_t crc, uint64_t nbytes) {
     return crc;
 }
 
-/* CRC-16 of [b0, b1) with two 64-byte loads in flight (g_crc16_t11 tables in LDS: 0.75
- * lookups per byte on whole lines, the byte table on the unaligned ends) */
 DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line offset o: bytes below h cleared */
     return h <= o ? ~0u : (h >= o + 4u ? 0u : (~0u << (8u * (h - o))));
 }
-#define CRC_LINES 4
-DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, const lds_u16 *T) {
-    uint32_t crc = 0; /* byte-swapped until the trailing bytes (crc16_step8le) */
-    /* whole lines from the one holding b0, its bytes below b0 taken as zeros (a CRC with
-     * init 0 stays 0 over leading zero bytes) */
-    const uint64_t p0 = b0 & ~(uint64_t)63u;
-    const uint32_t h = (uint32_t)(b0 & 63u);
+#define CRC_LINES 4 /* 64-byte lines in flight per lane: each lane walks its own frame */
+
+/* Zero test of the CRC-16 remainder of [b0, b1), the frame with its footer (read_frame_'s
+ * check @0x10011a01: the footer equals the CRC of the frame bytes iff the CRC of frame + footer
+ * is zero), by arithmetic, with no tables (round 6).  P = x^16 + x^15 + x^2 + 1 = (x + 1) T with
+ * T = x^15 + x + 1, so M = 0 mod P iff M has even parity and M = 0 mod T.  The remainder mod
+ * T^4 = x^60 + x^4 + 1 (a multiple of T) costs five VALU per 32-bit word: with the state
+ * r = r1:r0 (60 bits; r1's top four bits are stale copies of bits alignbit already took),
+ * r x^32 + W = (r0 mod x^28) x^32 + W + H (x^4 + 1), H = r >> 28.  Leading zero bytes leave M
+ * unchanged and trailing ones multiply it by a power of x (invertible mod T), so whole 16-byte
+ * blocks with the bytes outside [b0, b1) cleared give the same verdict.  The 11-bit LDS tables
+ * this replaces cost 0.75 bank-conflicted lookups per byte on the CU's one LDS pipe. */
+DEV uint32_t byte_keep(int32_t lo, int32_t hi, int32_t w) { /* bytes 4w..4w+3 kept iff in [lo, hi) */
+    const int32_t a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
+    const uint32_t mlo = a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
+    const uint32_t mhi = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    return mlo & mhi;
+}
+struct CrcZ {
+    uint32_t r0, r1, px; /* remainder mod T^4; XOR of every word (parity) */
+};
+DEV void crcz_w(CrcZ &c, uint32_t le) { /* one little-endian stream word */
+    const uint32_t W = __builtin_bswap32(le);
+    const uint32_t H = __builtin_amdgcn_alignbit(c.r1, c.r0, 28);
+    const uint32_t n0 = W ^ H ^ (H << 4);
+    c.r1 = c.r0 ^ (H >> 28);
+    c.r0 = n0;
+}
+DEV void crcz_blk(CrcZ &c, uint4 v) {
+    c.px ^= v.x ^ v.y ^ v.z ^ v.w;
+    crcz_w(c, v.x);
+    crcz_w(c, v.y);
+    crcz_w(c, v.z);
+    crcz_w(c, v.w);
+}
+DEV bool crcz_zero(const CrcZ &c) {
+    if (__builtin_popcount(c.px) & 1) return false;
+    uint64_t v = ((uint64_t)(c.r1 & 0x0FFFFFFFu) << 32) | c.r0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { /* x^15 = x + 1: degree 59 -> 45 -> 31 -> 17 -> 14 */
+        const uint64_t h = v >> 15;
+        v = (v & 0x7FFFu) ^ h ^ (h << 1);
+    }
+    return v == 0;
+}
+/* the 64-byte line at q into the remainder, its bytes below h cleared (h = 0: whole line) */
+DEV void crcz_line(CrcZ &c, uint4 (&v)[4], uint32_t h) {
+    if (h) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            v[u].x &= st_hmask(h, 16u * u);
+            v[u].y &= st_hmask(h, 16u * u + 4u);
+            v[u].z &= st_hmask(h, 16u * u + 8u);
+            v[u].w &= st_hmask(h, 16u * u + 12u);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) crcz_blk(c, v[u]);
+}
+/* CRC-16 verdict of [b0, b1) with CRC_LINES 64-byte lines in flight per lane, continuing c,
+ * which already holds the lines [b0 & ~63, from) (from: a line boundary) */
+DEV bool st_crc16_ok(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, CrcZ c = CrcZ{0u, 0u, 0u},
+                     uint64_t from = 0) {
+    const uint64_t p0 = max(b0 & ~(uint64_t)63u, from);
+    const uint32_t h = p0 < b0 ? (uint32_t)(b0 & 63u) : 0u;
     const uint32_t nl = b1 > p0 ? (uint32_t)((b1 - p0) >> 6) : 0u;
-    uint64_t p = b0;
+    uint64_t p = p0;
     if (nl) {
-        /* CRC_LINES lines in flight per lane: each lane walks its own frame, so the loads of
-         * one line wait a full HBM latency; one line ahead left the loop latency-bound */
         const uint4 *q = (const uint4 *)(bytes + p0);
         uint4 buf[CRC_LINES][4];
 #pragma unroll
@@ -1859,10 +1853,7 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
             for (int d = 0; d < CRC_LINES; d++) {
                 if (i + d < nl) {
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        crc = crc16_step8le(crc, buf[d][u].x, buf[d][u].y, T);
-                        crc = crc16_step8le(crc, buf[d][u].z, buf[d][u].w, T);
-                    }
+                    for (int u = 0; u < 4; u++) crcz_blk(c, buf[d][u]);
                     const uint32_t j = min(i + d + CRC_LINES, nl - 1u);
 #pragma unroll
                     for (int u = 0; u < 4; u++) buf[d][u] = q[4u * j + u];
@@ -1870,21 +1861,28 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
             }
         }
         p = p0 + (uint64_t)nl * 64u;
-        /* the last partial line: whole 8-byte steps (loads issued together), then bytes */
-        const uint32_t n8 = (uint32_t)((b1 - p) >> 3);
-        const uint2 *q8 = (const uint2 *)(bytes + p);
-        uint2 t8[7];
-#pragma unroll
-        for (uint32_t i = 0; i < 7; i++) t8[i] = i < n8 ? q8[i] : make_uint2(0u, 0u);
-#pragma unroll
-        for (uint32_t i = 0; i < 7; i++)
-            if (i < n8) crc = crc16_step8le(crc, t8[i].x, t8[i].y, T);
-        p += 8u * n8;
     }
-    crc = crc16_unswap(crc);
-    /* trailing bytes: the byte table is w1's [22,32) field table at byte << 2 (stream byte 7) */
-    while (p < b1) { crc = ((crc << 8) ^ crc16_unswap(T[CRC_BYTE_OFF + ((((crc >> 8) ^ bytes[p]) & 0xffu) << CRC_BYTE_SH)])) & 0xffff; p++; }
-    return crc;
+    /* the rest, [p, b1): up to four 16-byte blocks (each starts below b1, so it lies inside the
+     * 16-byte-rounded allocation), bytes below b0 (a frame inside one line) or from b1 on cleared */
+    const uint32_t nr = (uint32_t)((b1 - p + 15u) >> 4);
+    uint4 t[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) t[i] = i < nr ? *(const uint4 *)(bytes + p + 16u * i) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        if (i < nr) {
+            const int64_t lo = (int64_t)b0 - (int64_t)(p + 16u * i), hi = (int64_t)b1 - (int64_t)(p + 16u * i);
+            const int32_t l32 = (int32_t)max(min(lo, (int64_t)16), (int64_t)0);
+            const int32_t h32 = (int32_t)max(min(hi, (int64_t)16), (int64_t)0);
+            uint4 v = t[i];
+            v.x &= byte_keep(l32, h32, 0);
+            v.y &= byte_keep(l32, h32, 1);
+            v.z &= byte_keep(l32, h32, 2);
+            v.w &= byte_keep(l32, h32, 3);
+            crcz_blk(c, v);
+        }
+    }
+    return crcz_zero(c);
 }
 
 /* Wave-cooperative CRC-16 of one byte range (the whole wave, coalesced 1 KB loads).
@@ -1896,12 +1894,6 @@ DEV uint32_t st_crc16(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b
  * zero (x is invertible mod P).  Bytes outside
  * [b0, b1) are masked to 0 (leading zeros leave a zero-initialised CRC at 0). */
 DEV uint32_t crc_mulk(uint32_t a, const lds_u16 *TK) { return TK[a & 0xffu] ^ TK[256u + (a >> 8)]; }
-DEV uint32_t byte_keep(int32_t lo, int32_t hi, int32_t w) { /* bytes 4w..4w+3 kept iff in [lo, hi) */
-    const int32_t a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
-    const uint32_t mlo = a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
-    const uint32_t mhi = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
-    return mlo & mhi;
-}
 DEV uint4 gld16(const uint8_t *p) { /* a global (not flat) 16-byte load */
     const u32x4 v = *(__attribute__((address_space(1))) const u32x4 *)(uintptr_t)p;
     return make_uint4(v.x, v.y, v.z, v.w);
@@ -3655,8 +3647,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ perm, uint32_t ablate) {
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t ST_SPG = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u; /* stores per 4 samples */
-    /* 16 KB: both channels' bitstream rings; in the tail, the 20 KB CRC-16 field tables */
-    __shared__ LDS_DMA_ALIGN uint32_t ring[(2 * ST_RD * RING_LANE_DW > CRC11_N / 2) ? 2 * ST_RD * RING_LANE_DW : CRC11_N / 2];
+    /* 16 KB: both channels' bitstream rings; 4 KB: the flush tile (20 KB, 8 waves per CU) */
+    __shared__ LDS_DMA_ALIGN uint32_t ring[2 * ST_RD * RING_LANE_DW + 1024]; /* the two rings, then the 4 KB flush tile */
     static_assert((ST_RD * RING_LANE_DW * 4) % 1024 == 0, "channel 1's ring base must stay 1 KiB aligned (LDS-DMA)");
     const uint32_t lane = threadIdx.x;
     const uint32_t slot = blockIdx.x * 64u + lane;
@@ -3706,9 +3698,10 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     const bool as_uni = !any_lane(ok && as != as_u);
     /* the fused chunks' compile-time assignment: one per wave, no wasted bits */
     const int as_fix = (as_uni && !anyw && as_u <= 3u) ? (int)as_u : -1;
-    /* the flush's staging: the 4 KB past the two rings (the CRC tables' share of the LDS), not
+    /* the flush's staging: the 4 KB past the two rings, not
      * an LDS-DMA target */
     lds_u32x4 *stg = (lds_u32x4 *)((lds_u32 *)ring + 2u * ST_RD * RING_LANE_DW);
+    static_assert(sizeof(ring) >= (2 * ST_RD * RING_LANE_DW + 1024) * 4, "the flush's 4 KB staging tile lies past the two rings");
 
     uint32_t mybs = ok ? bs : 0u;
     for (int o = 32; o > 0; o >>= 1) mybs = max(mybs, (uint32_t)__shfl_xor(mybs, o));
@@ -3825,7 +3818,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
             uint64_t run = (valid && sto) ? (uint64_t)(uintptr_t)(dst + (uint64_t)n0 * 4u) : 0ull;
             /* timing ablation 0x10000000: the same stores into one 64 KB window per XCD (an
              * L2-resident footprint: the HBM write traffic without the instructions); wrong PCM */
-            if ((ablate & 0x10000000u) && run)
+            if ((ablate & 0x10000000u) && run && out_bytes >= (1u << 20)) /* the window needs 513 KB */
                 run = (uint64_t)(uintptr_t)(out + (uint64_t)(blockIdx.x & 7u) * 65536u + lane * 1024u + ((n0 * 4u) & 1023u));
             const uint32_t rlo = (uint32_t)run, rhi = (uint32_t)(run >> 32);
             const uint32_t fr = lane & 31u, ul = lane & 7u;
@@ -3880,28 +3873,15 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
         if (br_pos(z1.b) > limit) ok = false;
         resume = br_pos(z1.b);
     }
-    /* CRC-16 of the frame bytes (read_frame_'s footer check @0x10011a01).  Round 5: the tail is
-     * 19% of this kernel on C2 (ablation 1), 7 points of it the re-read of the frame (ablation
-     * 0x40000000: the same work on L2-resident bytes).  A separate pass ahead of the decode
-     * (each frame over [offset, next offset), a wave per frame with 1 KB loads, the decode
-     * taking its verdict when the frame ends there) cost more than it saved: 2.2 ms against
-     * 1.7 ms at C2's 1,024 batches, 5 TB/s for the 11 GB, and no overlap with k_parse on a
-     * second stream. */
+    /* CRC-16 of the frame bytes (read_frame_'s footer check @0x10011a01), by the table-free
+     * zero test over frame + footer (st_crc16_ok; round 6: 10.8 -> 10.5 ms on C2 against round
+     * 5's 11-bit LDS tables, same box).  The tail is bound by the re-read: every wave of a CU
+     * reaches it together, so the 11 GB go at the HBM rate with no decode beside them (no CRC at
+     * all: 8.6 ms).  Keeping the remainder running inside the chunk loop instead (one line per
+     * refill point through the staging tile) needs ~6 more live VGPRs; at the 256 already in use
+     * the loop spilled (20-89 VGPRs) and the launch took 20 ms: dropped. */
     uint32_t crc = crc_read;
-    const bool need = ok && !(ablate & 1u);
-    if (any_lane(need)) {
-        wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
-        lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
-        for (uint32_t i = lane; i < CRC_TAB_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
-        __syncthreads();
-        /* timing ablation 0x40000000: the same CRC work over a 1 MB window per XCD (L2-resident,
-         * each lane its own 16 KB: the re-read's HBM traffic without the work); result ignored */
-        const bool hotc = (ablate & 0x40000000u) != 0;
-        const uint8_t *cb = (const uint8_t *)words;
-        if (hotc) cb = cb + ((uint64_t)(blockIdx.x & 7u) * 64u + lane) * 16384u + (fi.frame_off & 63u) - fi.frame_off;
-        if (need) crc = st_crc16(cb, fi.frame_off, (hotc && end_byte - fi.frame_off > 16000u) ? fi.frame_off + 16000u : end_byte, T);
-        if (hotc) crc = crc_read;
-    }
+    if (ok && !(ablate & 1u) && !st_crc16_ok((const uint8_t *)words, fi.frame_off, end_byte + 2u)) ok = false;
     if (ok && crc != crc_read) ok = false;
     if (ok) {
         info[f].resume_bit = resume;
@@ -4259,8 +4239,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
                                                      bnf_frame_info *__restrict__ info,
                                                      const uint32_t *__restrict__ perm, uint32_t ablate) {
     constexpr uint32_t SPG = sw_stores8<FMT>();
-    /* 16 KB: both channels' bitstream rings; in the tail, the 20 KB CRC-16 field tables */
-    __shared__ LDS_DMA_ALIGN uint32_t ring[(2 * ST_RD * RING_LANE_DW > CRC11_N / 2) ? 2 * ST_RD * RING_LANE_DW : CRC11_N / 2];
+    /* 16 KB: both channels' bitstream rings; 4 KB: the flush tile (20 KB, 8 waves per CU) */
+    __shared__ LDS_DMA_ALIGN uint32_t ring[2 * ST_RD * RING_LANE_DW + 1024]; /* the two rings, then the 4 KB flush tile */
     const uint32_t lane = threadIdx.x;
     const uint32_t slot = blockIdx.x * 64u + lane;
     const uint32_t f = (perm && slot < nframes) ? perm[slot] : slot;
@@ -4281,7 +4261,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     uint8_t *dst = out + os * stride;
     /* timing ablation 0x10000000: every wave stores into one 64 KB window (same store
      * instructions, an L2-resident footprint); output is wrong */
-    const bool hot = (ablate & 0x10000000u) != 0;
+    const bool hot = (ablate & 0x10000000u) != 0 && out_bytes >= (1u << 20); /* the window needs 513 KB */
     if (hot) dst = out + (uint64_t)(blockIdx.x & 7u) * 65536u + lane * 1024u;
     const bool al = (((uintptr_t)dst) & 15u) == 0 && (FMT != BNF_OUT_PLANAR32 || (bs & 3u) == 0);
     const bool all_al = !any_lane(ok && !al); /* every run of the wave takes the 16-byte stores */
@@ -4317,6 +4297,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     const bool line = FMT == BNF_OUT_FILEREADER && sto && !hot && all_al && !(ablate & 0x20000000u) &&
                       !any_lane(ok && (((uintptr_t)dst) & 63u) != 0);
     lds_u32x4 *stg = (lds_u32x4 *)((lds_u32 *)ring + 2u * ST_RD * RING_LANE_DW);
+    static_assert(sizeof(ring) >= (2 * ST_RD * RING_LANE_DW + 1024) * 4, "the flush's 4 KB staging tile lies past the two rings");
     static_assert(sizeof(ring) >= (2u * ST_RD * RING_LANE_DW + 1024u) * 4u, "line slots past the rings");
     SwLn q;
     SwRuns runs;
@@ -4455,14 +4436,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
         resume = br_pos(z1.b);
     }
     uint32_t crc = crc_read;
-    const bool need = ok && !(ablate & 1u);
-    if (any_lane(need)) {
-        wait_vm(); /* ring DMAs still in flight must land before the tables overwrite the ring */
-        lds_u16 *T = (lds_u16 *)(lds_u32 *)ring;
-        for (uint32_t i = lane; i < CRC_TAB_N / 2u; i += 64u) ((lds_u32 *)ring)[i] = ((const uint32_t *)g_crc16_t11)[i];
-        __syncthreads();
-        if (need) crc = st_crc16((const uint8_t *)words, fi.frame_off, end_byte, T);
-    }
+    /* the table-free zero test over frame + footer (round 6: 9.40 -> 9.23 ms on C3, same box) */
+    if (ok && !(ablate & 1u) && !st_crc16_ok((const uint8_t *)words, fi.frame_off, end_byte + 2u)) ok = false;
     if (ok && crc != crc_read) ok = false;
     if (ok) {
         info[f].resume_bit = resume;
@@ -4496,39 +4471,6 @@ static hipError_t upload_tables(const uint8_t *crc8, const uint16_t *crc16x8, co
     if (e != hipSuccess) return e;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_tab), crc16x8, 8 * 256 * sizeof(uint16_t));
     if (e != hipSuccess) return e;
-    { /* field tables (crc16_step8le) from the byte table (crc16x8[0]): the CRC of the 8-byte
-       * block holding v in bits [lo, lo + wd) of word j as loaded (LE bit p of word j = stream
-       * byte 4j + p / 8, bit p % 8 of that byte), stored byte-swapped */
-#if CRC_LAYOUT == 0
-        static const uint32_t lo[] = {0, 11, 22, 0, 11, 22}, wd[] = {11, 11, 10, 11, 11, 10}, wj[] = {0, 0, 0, 1, 1, 1};
-#elif CRC_LAYOUT == 1
-        static const uint32_t lo[] = {0, 11, 22, 28, 0, 6, 12, 18, 24, 30}, wd[] = {11, 11, 6, 4, 6, 6, 6, 6, 6, 2},
-                              wj[] = {0, 0, 0, 0, 1, 1, 1, 1, 1, 1};
-#else
-        static const uint32_t lo[] = {0, 6, 12, 18, 24, 30, 0, 6, 12, 18, 24, 30}, wd[] = {6, 6, 6, 6, 6, 2, 6, 6, 6, 6, 6, 2},
-                              wj[] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1};
-#endif
-        constexpr int NF = (int)(sizeof lo / sizeof lo[0]);
-        uint16_t t11[CRC_TAB_N];
-        uint32_t at = 0;
-        for (int fld = 0; fld < NF; fld++)
-            for (uint32_t v = 0; v < (1u << wd[fld]); v++) {
-                uint8_t blk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                for (uint32_t i = 0; i < wd[fld]; i++)
-                    if ((v >> i) & 1u) {
-                        const uint32_t p = lo[fld] + i;
-                        blk[4u * wj[fld] + p / 8u] |= (uint8_t)(1u << (p % 8u));
-                    }
-                uint32_t c = 0;
-                for (int by = 0; by < 8; by++) c = ((c << 8) ^ crc16x8[((c >> 8) ^ blk[by]) & 0xffu]) & 0xffffu;
-                t11[at++] = (uint16_t)(((c >> 8) | (c << 8)) & 0xffffu);
-            }
-        if (CRC_LAYOUT != 0) /* the byte table, byte-swapped like the fields */
-            for (uint32_t x = 0; x < 256u; x++) t11[at++] = (uint16_t)(((crc16x8[x] >> 8) | (crc16x8[x] << 8)) & 0xffffu);
-        if (at != CRC_TAB_N) return hipErrorInvalidValue;
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_t11), t11, sizeof t11);
-        if (e != hipSuccess) return e;
-    }
     return hipMemcpyToSymbol(HIP_SYMBOL(g_crc16_xpow), xpow, 40 * sizeof(uint16_t));
 }
 

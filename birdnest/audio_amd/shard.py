@@ -132,13 +132,17 @@ def gather_group_sizes(group_sizes, group=None, device=None):
 class GroupGather:
     """A gather of every rank's output to `dst` that starts while the ranks are still decoding
     ("overlap the gather chunk-wise with decode").  A rank decodes its
-    files in groups into consecutive slices of its output buffer and calls post(g, slice) as
-    soon as group g is enqueued; `dst` posted every receive up front, straight into the final
-    buffer at the rank-major, group-minor offset, so nothing is concatenated afterwards.
-    Under RCCL each post runs on the communicator's stream after the work already enqueued on
-    the current stream (that group's decode) and beside the decode of the next group; per
-    peer, sends and receives match in group order.  wait() completes everything; on `dst`
-    `out` then holds all ranks' bytes in rank order."""
+    output in groups (files, or frame ranges of a file) into consecutive slices of its output
+    buffer and calls post(g, slice) as soon as group g is enqueued.  Every post is one
+    batch_isend_irecv on every side, and the two sides post the same groups in the same order:
+    a sender posts its group g alone; `dst`, at its own post(g), posts the receives of group g
+    from every peer that has one (into the final buffer at the rank-major, group-minor offset,
+    so nothing is concatenated afterwards) and copies its own slice into place.  Groups `dst`
+    does not have are posted by wait(), before it waits.  Under RCCL each post runs on the
+    communicator's stream after the work already enqueued on the current stream (that group's
+    decode) and beside the decode of the next group; per peer, sends and receives pair up one
+    grouped call against one grouped call, in group order.  wait() completes everything; on
+    `dst` `out` then holds all ranks' bytes in rank order."""
 
     def __init__(self, sizes, like, group=None, dst: int = 0, out=None):
         import torch
@@ -146,40 +150,48 @@ class GroupGather:
 
         self.dist, self.group, self.dst = dist, group, dst
         self.rank = dist.get_rank(group)
-        world = dist.get_world_size(group)
+        self.world = dist.get_world_size(group)
         self.glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
         self.sizes = sizes
+        self.ngroups = max((len(x) for x in sizes), default=0)
         self.works = []
-        self.order = []  # (rank, group) of every post made by this rank, in post order
+        self.order = []  # every op this rank posted, in post order: ("recv"|"send"|"copy", rank, group)
+        self.posted = 0  # dst: groups whose receives are posted (0 .. posted-1)
         self.out = None
         if self.rank == dst:
-            total = sum(sum(s) for s in sizes)
+            total = sum(sum(x) for x in sizes)
             self.out = out if out is not None else torch.empty(total, dtype=like.dtype, device=like.device)
             self.base = []
             off = 0
-            for r in range(world):
+            for r in range(self.world):
                 row = []
-                for s in sizes[r]:
+                for n in sizes[r]:
                     row.append(off)
-                    off += s
+                    off += n
                 self.base.append(row)
-            ops = []
-            for r in range(world):
-                if r == self.rank:
-                    continue
-                for g, s in enumerate(sizes[r]):
-                    if s:
-                        ops.append(dist.P2POp(dist.irecv, self.out[self.base[r][g]:self.base[r][g] + s], self.glob(r), group))
-                        self.order.append(("recv", r, g))
-            if ops:
-                self.works += dist.batch_isend_irecv(ops)
+
+    def _post_recvs(self, g):
+        """dst: one grouped call with the receives of group g from every peer that has it."""
+        dist = self.dist
+        ops = []
+        for r in range(self.world):
+            if r != self.rank and g < len(self.sizes[r]) and self.sizes[r][g]:
+                b, n = self.base[r][g], self.sizes[r][g]
+                ops.append(dist.P2POp(dist.irecv, self.out[b:b + n], self.glob(r), self.group))
+                self.order.append(("recv", r, g))
+        if ops:
+            self.works += dist.batch_isend_irecv(ops)
 
     def post(self, g, part):
         """Group g of this rank (its bytes, in this rank's output order) is enqueued: send it
-        (or, on `dst`, copy it into place)."""
+        (on `dst`: receive every peer's group g and copy this one into place)."""
         if self.rank == self.dst:
+            while self.posted <= g:
+                self._post_recvs(self.posted)
+                self.posted += 1
             if part.numel():
-                self.out[self.base[self.rank][g]:self.base[self.rank][g] + part.numel()].copy_(part, non_blocking=True)
+                b = self.base[self.rank][g]
+                self.out[b:b + part.numel()].copy_(part, non_blocking=True)
             self.order.append(("copy", self.rank, g))
             return
         if part.numel():
@@ -188,7 +200,27 @@ class GroupGather:
         self.order.append(("send", self.rank, g))
 
     def wait(self):
+        if self.rank == self.dst:
+            while self.posted < self.ngroups:
+                self._post_recvs(self.posted)
+                self.posted += 1
         for w in self.works:
             w.wait()
         self.works = []
         return self.out
+
+
+def frame_groups(nframes_per_file, groups_per_file):
+    """Frame ranges [f0, f1) for GroupGather groups: each file's frames cut into up to
+    `groups_per_file` near-equal contiguous ranges (a file with fewer frames gets fewer), in
+    file order; returns (ranges, file index of each range)."""
+    out, owner, f0 = [], [], 0
+    for i, n in enumerate(nframes_per_file):
+        k = max(1, min(int(groups_per_file), int(n))) if n else 1
+        cuts = [f0 + (n * j) // k for j in range(k + 1)]
+        for a, b in zip(cuts, cuts[1:]):
+            if b > a or n == 0:
+                out.append((a, b))
+                owner.append(i)
+        f0 += n
+    return out, owner

@@ -179,7 +179,9 @@ BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d_bytes, uin
 
 /* Timing experiments only: skip parts of the kernels (bit0 CRC-16, bit1 PCM stores,
  * bit2 restore, bit3 Rice decode, bit4 subframe walk).  Output is wrong while set.
- * Exception: bit 0x800 only routes every k_decode chunk through the generic path (exact). */
+ * Exception: bit 0x800 only routes every k_decode chunk through the generic path (exact).
+ * Bit 0x10000000 aims k_decode_st's / k_decode_sw's PCM stores at a 513 KB window at the
+ * start of d_out (an L2-resident footprint); it is ignored when out_bytes < 1 MiB. */
 BNFLAC_API void bnflac_debug_set_ablate(uint32_t flags);
 /* Development / test switch: parse kernel (-1 auto, 0 lane-per-frame k_parse, 1 wave-per-frame
  * k_parse_wave); both write identical records. */

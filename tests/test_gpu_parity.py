@@ -135,6 +135,41 @@ def test_config_batch_vs_oracle_and_source(gpu, cfg, decode_mode):
     assert np.array_equal(pcm, oracle.interleave(ev, opcm))
 
 
+_C4_FULL = {}
+
+
+def _c4_full():
+    """BASELINE C4 at its full shape: 4,096 frames, variable blocksize 192-16,384, CONSTANT /
+    VERBATIM / FIXED / LPC up to order 32 (the generator takes ~15 s: encoded once per module)."""
+    if not _C4_FULL:
+        from birdnest.audio_amd import synth
+        p = synth.config("C4")
+        assert p.nframes == 4096 and p.bs_max == 16384
+        _C4_FULL["s"] = synth.encode(p)
+    return _C4_FULL["s"]
+
+
+@pytest.mark.parametrize("fmt_name", ["FLACDECODER", "INTERLEAVED32"])
+def test_c4_full_size_vs_source(gpu, fmt_name):
+    """C4 as the bench decodes it (default dispatch: k_decode_st, k_decode<8|16|32> by class,
+    the W16/W32 side grids), at full size: every record OK with a checked CRC-16, and the PCM
+    equal to the generator's source, including the 16,384-sample LPC-32 frames at the long tail
+    of the decode order."""
+    torch, libflac, _ = gpu
+    s = _c4_full()
+    data = s.data.tobytes()
+    assert int(np.diff(np.asarray(s.frame_offsets)).max()) > 0
+    fmt = getattr(libflac, "OUT_" + fmt_name)
+    out, info, sp = _decode_batch(gpu, data, s.frame_offsets, fmt)
+    assert len(info) == 4096
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    assert int(info["blocksize"].max()) == 16384 and int(info["blocksize"].min()) <= 256
+    if fmt_name == "FLACDECODER":
+        assert out.tobytes() == s.pcm.astype("<i2").tobytes()
+    else:
+        assert np.array_equal(out.view("<i4").reshape(-1, 2), s.pcm)
+
+
 @pytest.mark.parametrize("order,prec,stereo", [(2, 15, 0), (3, 0, 3), (4, 12, 0), (8, 15, 1), (8, 0, 2),
                                                 (12, 15, 3), (16, 0, 0), (32, 15, 3), (32, 0, 0)])
 @pytest.mark.parametrize("decode_mode", [0, 2], indirect=True)

@@ -200,16 +200,13 @@ def _group_worker(rank, world, port, groups, result_q):
         dist.destroy_process_group()
 
 
-def test_group_gather_overlaps_decode_three_ranks():
-    """shard.GroupGather (the C5 flow's in-job overlap): every rank posts its groups as they
-    are decoded; rank 0 has every receive posted up front, into the final buffer at the
-    rank-major, group-minor offsets.  Ragged groups, an empty group, a rank with one group."""
+def _run_group_gather(groups):
     import torch.multiprocessing as mp
-    groups = [[300, 0, 1201], [4096, 17], [999]]
+    world = len(groups)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_group_worker, args=(r, 3, port, groups, q)) for r in range(3)]
+    procs = [ctx.Process(target=_group_worker, args=(r, world, port, groups, q)) for r in range(world)]
     for pr in procs:
         pr.start()
     got, order = q.get(timeout=120)
@@ -219,4 +216,31 @@ def test_group_gather_overlaps_decode_three_ranks():
     want = b"".join(bytes((i + r * 31 + g * 7) % 253 for i in range(n)) for r, gs in enumerate(groups)
                     for g, n in enumerate(gs))
     assert got == want
-    assert order == [("recv", 1, 0), ("recv", 1, 1), ("recv", 2, 0), ("copy", 0, 0), ("copy", 0, 1), ("copy", 0, 2)]
+    return order
+
+
+def test_group_gather_overlaps_decode_three_ranks():
+    """shard.GroupGather (the C5 flow's in-job overlap): every rank posts its groups as they
+    are decoded, each group as one grouped call on both sides: rank 0's post(g) receives group
+    g from every peer that has one (into the final buffer at the rank-major, group-minor
+    offsets) and copies its own.  Ragged groups, an empty group, a rank with one group."""
+    order = _run_group_gather([[300, 0, 1201], [4096, 17], [999]])
+    assert order == [("recv", 1, 0), ("recv", 2, 0), ("copy", 0, 0), ("recv", 1, 1), ("copy", 0, 1), ("copy", 0, 2)]
+
+
+def test_group_gather_dst_with_fewer_groups_two_ranks():
+    """Sub-file groups of uneven counts: rank 0 has one group, rank 1 four (frame ranges of its
+    file); wait() posts the receives of the groups rank 0 never reached, in group order."""
+    order = _run_group_gather([[512], [100, 100, 0, 37]])
+    assert order == [("recv", 1, 0), ("copy", 0, 0), ("recv", 1, 1), ("recv", 1, 3)]
+
+
+def test_frame_groups_cover_every_frame_in_order():
+    for nf, k in (([469] * 3, 4), ([5, 0, 1], 3), ([7], 1), ([2], 8)):
+        ranges, owner = shard.frame_groups(nf, k)
+        flat = [f for a, b in ranges for f in range(a, b)]
+        assert flat == list(range(sum(nf)))
+        starts = [0] + list(np.cumsum(nf))
+        for (a, b), i in zip(ranges, owner):
+            assert starts[i] <= a <= b <= starts[i + 1]
+        assert all(sum(1 for o in owner if o == i) <= max(1, k) for i in range(len(nf)))
