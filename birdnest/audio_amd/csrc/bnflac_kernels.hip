@@ -773,6 +773,190 @@ DEV uint32_t parse_subframe_head(R &b, uint32_t bps, uint32_t bs, uint64_t limit
     return br_pos(b) > limit ? BNF_ST_TRUNC : BNF_ST_OK;
 }
 
+DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line offset o: bytes below h cleared */
+    return h <= o ? ~0u : (h >= o + 4u ? 0u : (~0u << (8u * (h - o))));
+}
+/* ------------------------------------------------- CRC-16 remainder arithmetic
+ * (the table-free zero test, st_crc16_ok below, and k_parse's prefix of it) */
+struct CrcZ {
+    uint32_t r0, r1, px; /* remainder mod T^4; XOR of every word (parity) */
+};
+DEV void crcz_w(CrcZ &c, uint32_t le) { /* one little-endian stream word */
+    const uint32_t W = __builtin_bswap32(le);
+    const uint32_t H = __builtin_amdgcn_alignbit(c.r1, c.r0, 28);
+    const uint32_t n0 = W ^ H ^ (H << 4);
+    c.r1 = c.r0 ^ (H >> 28);
+    c.r0 = n0;
+}
+DEV void crcz_blk(CrcZ &c, uint4 v) {
+    c.px ^= v.x ^ v.y ^ v.z ^ v.w;
+    crcz_w(c, v.x);
+    crcz_w(c, v.y);
+    crcz_w(c, v.z);
+    crcz_w(c, v.w);
+}
+/* k_parse's part of a 2-channel frame's CRC-16 (round 6).  The decode kernels' tail re-reads
+ * the whole frame for the CRC-16, and every wave of a CU reaches its tail together, so those
+ * bytes go at the HBM rate with nothing beside them.  k_parse walks subframe 0 anyway: its ring
+ * holds those bytes, so it folds every whole 64-byte line before subframe 1's line into the
+ * same T^4 remainder (from the ring while the line is one of its two, else one reload, L2-warm),
+ * one 16-byte block at a time (three live state words: k_parse's occupancy is LDS-bound at 5
+ * waves per SIMD, ~100 VGPRs), and the decode tail continues from there, re-reading only the
+ * rest of the frame. */
+struct CrcP {
+    CrcZ z;      /* remainder mod T^4 and parity of lines [frame_off / 64, wc) */
+    uint32_t wc; /* next line to fold (absolute 64-byte line index); ~0: no prefix for this frame */
+};
+DEV void crcp_fold(CrcP &c, const u32x4 (&v)[4]) {
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) crcz_blk(c.z, make_uint4(v[i].x, v[i].y, v[i].z, v[i].w));
+    c.wc++;
+}
+/* fold the lines wholly before the cursor (whole wave; the ring's two lines are
+ * [iend / 4 - 2, iend / 4), landed once behind the cursor).  The frame's first line is folded
+ * before the walk (parse_frame), so these are whole lines. */
+DEV void crcp_hook(CrcP &c, const BR &b, uint32_t lane) {
+    const uint32_t cl = (uint32_t)(br_pos(b) >> 9);
+    while (any_lane(c.wc < cl)) {
+        if (c.wc < cl) {
+            const uint32_t L = c.wc;
+            u32x4 v[4];
+            if (L + 2u >= (b.iend >> 2)) {
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++)
+                    v[i] = lds_ld128((const lds_u32x4 *)(b.ring + (((L & 1u) * 4u + i) * RING_LANE_DW) + lane * 4u));
+                lds_sync();
+            } else { /* overwritten by a refill: read it again */
+                const u32x4 *g = (const u32x4 *)((const uint8_t *)b.w + (uint64_t)L * 64u);
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++) v[i] = g[i];
+            }
+            crcp_fold(c, v);
+        }
+    }
+}
+
+#define CRC_LINES 4 /* 64-byte lines in flight per lane: each lane walks its own frame */
+
+/* Zero test of the CRC-16 remainder of [b0, b1), the frame with its footer (read_frame_'s
+ * check @0x10011a01: the footer equals the CRC of the frame bytes iff the CRC of frame + footer
+ * is zero), by arithmetic, with no tables (round 6).  P = x^16 + x^15 + x^2 + 1 = (x + 1) T with
+ * T = x^15 + x + 1, so M = 0 mod P iff M has even parity and M = 0 mod T.  The remainder mod
+ * T^4 = x^60 + x^4 + 1 (a multiple of T) costs five VALU per 32-bit word: with the state
+ * r = r1:r0 (60 bits; r1's top four bits are stale copies of bits alignbit already took),
+ * r x^32 + W = (r0 mod x^28) x^32 + W + H (x^4 + 1), H = r >> 28.  Leading zero bytes leave M
+ * unchanged and trailing ones multiply it by a power of x (invertible mod T), so whole 16-byte
+ * blocks with the bytes outside [b0, b1) cleared give the same verdict.  The 11-bit LDS tables
+ * this replaces cost 0.75 bank-conflicted lookups per byte on the CU's one LDS pipe. */
+DEV uint32_t byte_keep(int32_t lo, int32_t hi, int32_t w) { /* bytes 4w..4w+3 kept iff in [lo, hi) */
+    const int32_t a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
+    const uint32_t mlo = a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
+    const uint32_t mhi = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    return mlo & mhi;
+}
+DEV bool crcz_zero(const CrcZ &c) {
+    if (__builtin_popcount(c.px) & 1) return false;
+    uint64_t v = ((uint64_t)(c.r1 & 0x0FFFFFFFu) << 32) | c.r0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { /* x^15 = x + 1: degree 59 -> 45 -> 31 -> 17 -> 14 */
+        const uint64_t h = v >> 15;
+        v = (v & 0x7FFFu) ^ h ^ (h << 1);
+    }
+    return v == 0;
+}
+/* the 64-byte line at q into the remainder, its bytes below h cleared (h = 0: whole line) */
+DEV void crcz_line(CrcZ &c, uint4 (&v)[4], uint32_t h) {
+    if (h) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            v[u].x &= st_hmask(h, 16u * u);
+            v[u].y &= st_hmask(h, 16u * u + 4u);
+            v[u].z &= st_hmask(h, 16u * u + 8u);
+            v[u].w &= st_hmask(h, 16u * u + 12u);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) crcz_blk(c, v[u]);
+}
+/* CRC-16 verdict of [b0, b1) with NL 64-byte lines in flight per lane, continuing c, which
+ * already holds the lines [b0 & ~63, from) (from: a line boundary) */
+template <int NL = CRC_LINES>
+DEV bool st_crc16_ok(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, CrcZ c = CrcZ{0u, 0u, 0u},
+                     uint64_t from = 0) {
+    const uint64_t p0 = max(b0 & ~(uint64_t)63u, from);
+    const uint32_t h = p0 < b0 ? (uint32_t)(b0 & 63u) : 0u;
+    const uint32_t nl = b1 > p0 ? (uint32_t)((b1 - p0) >> 6) : 0u;
+    uint64_t p = p0;
+    if (nl) {
+        const uint4 *q = (const uint4 *)(bytes + p0);
+        uint4 buf[NL][4];
+#pragma unroll
+        for (int d = 0; d < NL; d++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) buf[d][u] = q[4u * min((uint32_t)d, nl - 1u) + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            buf[0][u].x &= st_hmask(h, 16u * u);
+            buf[0][u].y &= st_hmask(h, 16u * u + 4u);
+            buf[0][u].z &= st_hmask(h, 16u * u + 8u);
+            buf[0][u].w &= st_hmask(h, 16u * u + 12u);
+        }
+        for (uint32_t i = 0; i < nl; i += NL) {
+#pragma unroll
+            for (int d = 0; d < NL; d++) {
+                if (i + d < nl) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) crcz_blk(c, buf[d][u]);
+                    const uint32_t j = min(i + d + NL, nl - 1u);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) buf[d][u] = q[4u * j + u];
+                }
+            }
+        }
+        p = p0 + (uint64_t)nl * 64u;
+    }
+    /* the rest, [p, b1): up to four 16-byte blocks (each starts below b1, so it lies inside the
+     * 16-byte-rounded allocation), bytes below b0 (a frame inside one line) or from b1 on cleared */
+    const uint32_t nr = (uint32_t)((b1 - p + 15u) >> 4);
+    uint4 t[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) t[i] = i < nr ? *(const uint4 *)(bytes + p + 16u * i) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        if (i < nr) {
+            const int64_t lo = (int64_t)b0 - (int64_t)(p + 16u * i), hi = (int64_t)b1 - (int64_t)(p + 16u * i);
+            const int32_t l32 = (int32_t)max(min(lo, (int64_t)16), (int64_t)0);
+            const int32_t h32 = (int32_t)max(min(hi, (int64_t)16), (int64_t)0);
+            uint4 v = t[i];
+            v.x &= byte_keep(l32, h32, 0);
+            v.y &= byte_keep(l32, h32, 1);
+            v.z &= byte_keep(l32, h32, 2);
+            v.w &= byte_keep(l32, h32, 3);
+            crcz_blk(c, v);
+        }
+    }
+    return crcz_zero(c);
+}
+/* The CRC-16 hand-off to the decode tails, 8 words per frame (crcp[8f..8f+7]): r0, r1 |
+ * parity << 31 of a prefix, the lines it holds + 1 (0: none), frame_off's low word (a check);
+ * the span to the next frame's offset (0: none), the verdict over that span, frame_off's low
+ * word.  Written by k_parse (crc_mode 1: the prefix; 2: both). */
+#define CRCP_WORDS 8u
+/* the decode tails' CRC-16 verdict of the frame [b0, b1): the hand-off's verdict when the
+ * frame ends where the next one starts, else its prefix continued, else the whole frame */
+DEV bool st_crc16_frame(const uint8_t *__restrict__ bytes, const uint32_t *__restrict__ crcp, uint32_t f, uint64_t b0,
+                        uint64_t b1) {
+    if (crcp) {
+        const u32x4 v = *(const u32x4 *)(crcp + CRCP_WORDS * (uint64_t)f + 4u);
+        if (v.x && v.z == (uint32_t)b0 && b0 + v.x == b1) return v.y != 0u;
+        const u32x4 q = *(const u32x4 *)(crcp + CRCP_WORDS * (uint64_t)f);
+        const uint64_t from = ((b0 >> 6) + q.z - 1u) * 64u;
+        if (q.z && q.w == (uint32_t)b0 && from <= b1)
+            return st_crc16_ok(bytes, b0, b1, CrcZ{q.x, q.y & 0x0FFFFFFFu, q.y >> 31}, from);
+    }
+    return st_crc16_ok(bytes, b0, b1);
+}
+
 /* One step of k_parse's residual walk: up to two Rice codewords of the current partition
  * (parameter k; km = 31 - k, k1 = k + 1).  Two codewords per 32-bit window when both fit:
  * the second's prefix is counted in the window shifted past the first (zeros shifted in
@@ -839,8 +1023,10 @@ DEV void pkb_step(BR &b, uint32_t k1, uint32_t &nf, uint32_t laneb) {
     b.wi += (uint32_t)c;
     b.ra = (((b.ra | 0x3F3u) + (uint32_t)c) & 0x1C0Cu) | laneb;
 }
-template <bool BULK> /* BULK: with the bulk iterations (a separate instance: the plain loop keeps its registers) */
-DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate) {
+/* BULK: with the bulk iterations (a separate instance: the plain loop keeps its registers);
+ * CP: fold the CRC-16 prefix (crcp_hook) before each refill */
+template <bool BULK, bool CP>
+DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate, CrcP &cp) {
     const uint32_t parts = 1u << h.porder;
     const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
     const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
@@ -851,12 +1037,14 @@ DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit
     while (any_lane(rem != 0u || p < parts)) {
         if (BULK) {
             if (__builtin_amdgcn_readfirstlane(since) >= 12u && !(ablate & 32u)) { /* every 12-14 steps */
+                if (CP) crcp_hook(cp, b, lane); /* the lines behind the cursor, before the refill overwrites them */
                 br_refill(b);
                 pk_resync(b, lane);
                 since = 0;
             }
             since += 2u;
         } else if ((__builtin_amdgcn_readfirstlane(since++) & 7u) == 0u && !(ablate & 32u)) { /* every 16 steps */
+            if (CP) crcp_hook(cp, b, lane);
             br_refill(b);
             pk_resync(b, lane);
         }
@@ -962,10 +1150,11 @@ DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit
 /* The bulk instance when every lane's first partition has a small Rice parameter (k <= 9:
  * pairs of codewords fit a window; C2's k = 8), peeked at the cursor, which sits on that
  * parameter; the plain loop otherwise (C3 / C4: larger parameters, short partitions). */
-DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate) {
+template <bool CP>
+DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate, CrcP &cp) {
     const uint32_t k0 = br_peek(b) >> (h.rice2 ? 27u : 28u);
-    if (!any_lane(k0 > 9u)) return skip_residual_t<true>(b, h, bs, limit, ablate);
-    return skip_residual_t<false>(b, h, bs, limit, ablate);
+    if (!any_lane(k0 > 9u)) return skip_residual_t<true, CP>(b, h, bs, limit, ablate, cp);
+    return skip_residual_t<false, CP>(b, h, bs, limit, ablate, cp);
 }
 
 /* ------------------------------------------- wave-cooperative Rice boundary scan */
@@ -1436,10 +1625,11 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 static_assert(PARSE_RD == 8, "pk_ra and the walk's pair steps (slot masks 0x3F3 / 0x1C0C, slot bits 10-12) assume an 8-slot ring");
 /* One lane per candidate frame: header + cursor walk over subframes 0..C-2.  Also
  * flags frames with an LPC order above 8 (they go to k_decode<32>). */
+template <int CPM> /* the CRC-16 hand-off (crc_mode): 1 the prefix, 2 the prefix and the verdict */
 DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const uint64_t *__restrict__ frame_offs,
                      uint32_t nframes, const bnf_stream_params &sp, const uint64_t *__restrict__ out_sample_in,
                      uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate, lds_u32 *ring,
-                     uint32_t f) {
+                     uint32_t f, uint32_t *__restrict__ crcp) {
     if (f >= nframes) return;
     bnf_frame_info fi;
     fi.status = BNF_ST_OK;
@@ -1464,8 +1654,28 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
     const uint64_t fbit = fi.frame_off * 8u;
     BR b;
     br_init(b, words, nbytes, ring, threadIdx.x, PARSE_RD);
+    CrcP cp; /* the CRC-16 prefix of a 2-channel frame (crcp != nullptr: the batch decode's hand-off) */
+    cp.z = CrcZ{0u, 0u, 0u};
+    cp.wc = ~0u;
     uint32_t st = parse_header(b, fbit, limit, sp, fi);
     if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
+    if (CPM && crcp != nullptr && st == BNF_ST_OK && fi.channels == 2u && !(ablate & 16u)) {
+        /* the frame's first line, its bytes below frame_off cleared (L2-warm: the ring's
+         * refill just read it) */
+        const uint32_t h = (uint32_t)(fi.frame_off & 63u);
+        const u32x4 *g = (const u32x4 *)((const uint8_t *)words + (fi.frame_off & ~(uint64_t)63u));
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            v[i] = g[i];
+            v[i].x &= st_hmask(h, 16u * i);
+            v[i].y &= st_hmask(h, 16u * i + 4u);
+            v[i].z &= st_hmask(h, 16u * i + 8u);
+            v[i].w &= st_hmask(h, 16u * i + 12u);
+        }
+        cp.wc = (uint32_t)(fi.frame_off >> 6);
+        crcp_fold(cp, v);
+    }
     if (st == BNF_ST_OK) {
         /* position in the batch output */
         uint64_t sample;
@@ -1498,8 +1708,10 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
             if (st == BNF_ST_OK) {
                 if (h.type == T_LPC) maxorder = max(maxorder, h.order);
                 raw = raw || h.type == T_CONST || h.type == T_VERB;
+                /* the prefix only for the frames k_decode_st / k_decode_sw can take */
+                if (!(h.type == T_FIXED || h.type == T_LPC) || h.order > (fi.bps > 16u ? 12u : 8u)) cp.wc = ~0u;
                 if (h.type == T_VERB) br_skip(b, (uint64_t)h.bps * fi.blocksize);
-                else if (h.type == T_FIXED || h.type == T_LPC) st = skip_residual(b, h, fi.blocksize, limit, ablate);
+                else if (h.type == T_FIXED || h.type == T_LPC) st = skip_residual<CPM != 0>(b, h, fi.blocksize, limit, ablate, cp);
                 if (st == BNF_ST_OK && br_pos(b) > limit) st = BNF_ST_TRUNC;
             }
             if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
@@ -1523,6 +1735,24 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
 #pragma unroll
     for (int c = 0; c < 8; c++) fi.sub_start[c] = ss[c];
     info[f] = fi;
+    if (CPM && crcp) { /* the hand-off (CRCP_WORDS) to the k_decode_st / k_decode_sw tails */
+        u32x4 o = u32x4{0u, 0u, 0u, 0u}, o2 = u32x4{0u, 0u, 0u, 0u};
+        const uint32_t l1 = (uint32_t)(br_pos(b) >> 9); /* subframe 1's line */
+        if (cp.wc != ~0u && cp.wc <= l1 && st == BNF_ST_OK) {
+            crcp_hook(cp, b, threadIdx.x & 63u); /* every line before subframe 1's line */
+            o = u32x4{cp.z.r0, (cp.z.r1 & 0x0FFFFFFFu) | ((uint32_t)(__builtin_popcount(cp.z.px) & 1) << 31),
+                      cp.wc - (uint32_t)(fi.frame_off >> 6) + 1u, (uint32_t)fi.frame_off};
+            /* the rest up to the next frame's offset: where a frame of a contiguous batch ends
+             * (frame + footer), so its tail need not read the frame again */
+            const uint64_t nx = CPM == 2 && f + 1u < nframes ? frame_offs[f + 1u] : 0u;
+            if (CPM == 2 && nx > (uint64_t)l1 * 64u && nx <= nbytes && nx - fi.frame_off < (1u << 24))
+                o2 = u32x4{(uint32_t)(nx - fi.frame_off),
+                           st_crc16_ok<2>((const uint8_t *)words, fi.frame_off, nx, cp.z, (uint64_t)l1 * 64u) ? 1u : 0u,
+                           (uint32_t)fi.frame_off, 0u};
+        }
+        *(u32x4 *)(crcp + CRCP_WORDS * (uint64_t)f) = o;
+        *(u32x4 *)(crcp + CRCP_WORDS * (uint64_t)f + 4u) = o2;
+    }
 }
 
 #endif /* BNF_TU == 0 */
@@ -1764,126 +1994,6 @@ DEV uint32_t crc16_shift(uint32_t crc, uint64_t nbytes) {
     return crc;
 }
 
-DEV uint32_t st_hmask(uint32_t h, uint32_t o) { /* little-endian dword at line offset o: bytes below h cleared */
-    return h <= o ? ~0u : (h >= o + 4u ? 0u : (~0u << (8u * (h - o))));
-}
-#define CRC_LINES 4 /* 64-byte lines in flight per lane: each lane walks its own frame */
-
-/* Zero test of the CRC-16 remainder of [b0, b1), the frame with its footer (read_frame_'s
- * check @0x10011a01: the footer equals the CRC of the frame bytes iff the CRC of frame + footer
- * is zero), by arithmetic, with no tables (round 6).  P = x^16 + x^15 + x^2 + 1 = (x + 1) T with
- * T = x^15 + x + 1, so M = 0 mod P iff M has even parity and M = 0 mod T.  The remainder mod
- * T^4 = x^60 + x^4 + 1 (a multiple of T) costs five VALU per 32-bit word: with the state
- * r = r1:r0 (60 bits; r1's top four bits are stale copies of bits alignbit already took),
- * r x^32 + W = (r0 mod x^28) x^32 + W + H (x^4 + 1), H = r >> 28.  Leading zero bytes leave M
- * unchanged and trailing ones multiply it by a power of x (invertible mod T), so whole 16-byte
- * blocks with the bytes outside [b0, b1) cleared give the same verdict.  The 11-bit LDS tables
- * this replaces cost 0.75 bank-conflicted lookups per byte on the CU's one LDS pipe. */
-DEV uint32_t byte_keep(int32_t lo, int32_t hi, int32_t w) { /* bytes 4w..4w+3 kept iff in [lo, hi) */
-    const int32_t a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
-    const uint32_t mlo = a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
-    const uint32_t mhi = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
-    return mlo & mhi;
-}
-struct CrcZ {
-    uint32_t r0, r1, px; /* remainder mod T^4; XOR of every word (parity) */
-};
-DEV void crcz_w(CrcZ &c, uint32_t le) { /* one little-endian stream word */
-    const uint32_t W = __builtin_bswap32(le);
-    const uint32_t H = __builtin_amdgcn_alignbit(c.r1, c.r0, 28);
-    const uint32_t n0 = W ^ H ^ (H << 4);
-    c.r1 = c.r0 ^ (H >> 28);
-    c.r0 = n0;
-}
-DEV void crcz_blk(CrcZ &c, uint4 v) {
-    c.px ^= v.x ^ v.y ^ v.z ^ v.w;
-    crcz_w(c, v.x);
-    crcz_w(c, v.y);
-    crcz_w(c, v.z);
-    crcz_w(c, v.w);
-}
-DEV bool crcz_zero(const CrcZ &c) {
-    if (__builtin_popcount(c.px) & 1) return false;
-    uint64_t v = ((uint64_t)(c.r1 & 0x0FFFFFFFu) << 32) | c.r0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) { /* x^15 = x + 1: degree 59 -> 45 -> 31 -> 17 -> 14 */
-        const uint64_t h = v >> 15;
-        v = (v & 0x7FFFu) ^ h ^ (h << 1);
-    }
-    return v == 0;
-}
-/* the 64-byte line at q into the remainder, its bytes below h cleared (h = 0: whole line) */
-DEV void crcz_line(CrcZ &c, uint4 (&v)[4], uint32_t h) {
-    if (h) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            v[u].x &= st_hmask(h, 16u * u);
-            v[u].y &= st_hmask(h, 16u * u + 4u);
-            v[u].z &= st_hmask(h, 16u * u + 8u);
-            v[u].w &= st_hmask(h, 16u * u + 12u);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) crcz_blk(c, v[u]);
-}
-/* CRC-16 verdict of [b0, b1) with CRC_LINES 64-byte lines in flight per lane, continuing c,
- * which already holds the lines [b0 & ~63, from) (from: a line boundary) */
-DEV bool st_crc16_ok(const uint8_t *__restrict__ bytes, uint64_t b0, uint64_t b1, CrcZ c = CrcZ{0u, 0u, 0u},
-                     uint64_t from = 0) {
-    const uint64_t p0 = max(b0 & ~(uint64_t)63u, from);
-    const uint32_t h = p0 < b0 ? (uint32_t)(b0 & 63u) : 0u;
-    const uint32_t nl = b1 > p0 ? (uint32_t)((b1 - p0) >> 6) : 0u;
-    uint64_t p = p0;
-    if (nl) {
-        const uint4 *q = (const uint4 *)(bytes + p0);
-        uint4 buf[CRC_LINES][4];
-#pragma unroll
-        for (int d = 0; d < CRC_LINES; d++)
-#pragma unroll
-            for (int u = 0; u < 4; u++) buf[d][u] = q[4u * min((uint32_t)d, nl - 1u) + u];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            buf[0][u].x &= st_hmask(h, 16u * u);
-            buf[0][u].y &= st_hmask(h, 16u * u + 4u);
-            buf[0][u].z &= st_hmask(h, 16u * u + 8u);
-            buf[0][u].w &= st_hmask(h, 16u * u + 12u);
-        }
-        for (uint32_t i = 0; i < nl; i += CRC_LINES) {
-#pragma unroll
-            for (int d = 0; d < CRC_LINES; d++) {
-                if (i + d < nl) {
-#pragma unroll
-                    for (int u = 0; u < 4; u++) crcz_blk(c, buf[d][u]);
-                    const uint32_t j = min(i + d + CRC_LINES, nl - 1u);
-#pragma unroll
-                    for (int u = 0; u < 4; u++) buf[d][u] = q[4u * j + u];
-                }
-            }
-        }
-        p = p0 + (uint64_t)nl * 64u;
-    }
-    /* the rest, [p, b1): up to four 16-byte blocks (each starts below b1, so it lies inside the
-     * 16-byte-rounded allocation), bytes below b0 (a frame inside one line) or from b1 on cleared */
-    const uint32_t nr = (uint32_t)((b1 - p + 15u) >> 4);
-    uint4 t[4];
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) t[i] = i < nr ? *(const uint4 *)(bytes + p + 16u * i) : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) {
-        if (i < nr) {
-            const int64_t lo = (int64_t)b0 - (int64_t)(p + 16u * i), hi = (int64_t)b1 - (int64_t)(p + 16u * i);
-            const int32_t l32 = (int32_t)max(min(lo, (int64_t)16), (int64_t)0);
-            const int32_t h32 = (int32_t)max(min(hi, (int64_t)16), (int64_t)0);
-            uint4 v = t[i];
-            v.x &= byte_keep(l32, h32, 0);
-            v.y &= byte_keep(l32, h32, 1);
-            v.z &= byte_keep(l32, h32, 2);
-            v.w &= byte_keep(l32, h32, 3);
-            crcz_blk(c, v);
-        }
-    }
-    return crcz_zero(c);
-}
 
 /* Wave-cooperative CRC-16 of one byte range (the whole wave, coalesced 1 KB loads).
  * Layout: 16-byte pieces counted back from e = round_up(b1, 16); lane l takes pieces
@@ -1950,18 +2060,17 @@ DEV void crc_tk_fill(lds_u16 *TK, uint32_t lane) {
 /* ============================================================== k_parse
  * One lane per frame (parse_frame: the lane-serial subframe walk), 64 frames per single-wave
  * workgroup, in the parse order when there is one. */
+template <int CPM>
 __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint64_t nbytes,
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
                                               uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate,
-                                              const uint32_t *__restrict__ perm) {
+                                              const uint32_t *__restrict__ perm, uint32_t *__restrict__ crcp) {
     __shared__ LDS_DMA_ALIGN uint32_t ring[PARSE_RD * RING_LANE_DW]; /* the bit ring */
     const uint32_t slot = blockIdx.x * 64u + threadIdx.x; /* parse order (launch_order<1>) */
-    parse_frame(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
-                (perm && slot < nframes) ? perm[slot] : slot);
+    parse_frame<CPM>(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
+                (perm && slot < nframes) ? perm[slot] : slot, crcp);
 }
-
-
 
 /* =========================================================== k_parse_wave
  * One wave per frame: the same record as parse_frame (header, subframe starts, decode class),
@@ -3644,7 +3753,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
                                                      uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                      uint8_t *__restrict__ out, uint64_t out_bytes,
                                                      bnf_frame_info *__restrict__ info,
-                                                     const uint32_t *__restrict__ perm, uint32_t ablate) {
+                                                     const uint32_t *__restrict__ perm, uint32_t ablate,
+                                                     const uint32_t *__restrict__ crcp) {
     constexpr bool STG = (FMT == BNF_OUT_FLACDECODER || FMT == BNF_OUT_FILEREADER);
     constexpr uint32_t ST_SPG = (FMT == BNF_OUT_INTERLEAVED32 || FMT == BNF_OUT_PLANAR32) ? 2u : 1u; /* stores per 4 samples */
     /* 16 KB: both channels' bitstream rings; 4 KB: the flush tile (20 KB, 8 waves per CU) */
@@ -3881,7 +3991,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
      * refill point through the staging tile) needs ~6 more live VGPRs; at the 256 already in use
      * the loop spilled (20-89 VGPRs) and the launch took 20 ms: dropped. */
     uint32_t crc = crc_read;
-    if (ok && !(ablate & 1u) && !st_crc16_ok((const uint8_t *)words, fi.frame_off, end_byte + 2u)) ok = false;
+    if (ok && !(ablate & 1u) && !st_crc16_frame((const uint8_t *)words, crcp, f, fi.frame_off, end_byte + 2u)) ok = false;
     if (ok && crc != crc_read) ok = false;
     if (ok) {
         info[f].resume_bit = resume;
@@ -4237,7 +4347,8 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
                                                      uint32_t nframes, bnf_stream_params sp, uint32_t chn_lanes,
                                                      uint8_t *__restrict__ out, uint64_t out_bytes,
                                                      bnf_frame_info *__restrict__ info,
-                                                     const uint32_t *__restrict__ perm, uint32_t ablate) {
+                                                     const uint32_t *__restrict__ perm, uint32_t ablate,
+                                                     const uint32_t *__restrict__ crcp) {
     constexpr uint32_t SPG = sw_stores8<FMT>();
     /* 16 KB: both channels' bitstream rings; 4 KB: the flush tile (20 KB, 8 waves per CU) */
     __shared__ LDS_DMA_ALIGN uint32_t ring[2 * ST_RD * RING_LANE_DW + 1024]; /* the two rings, then the 4 KB flush tile */
@@ -4437,7 +4548,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     }
     uint32_t crc = crc_read;
     /* the table-free zero test over frame + footer (round 6: 9.40 -> 9.23 ms on C3, same box) */
-    if (ok && !(ablate & 1u) && !st_crc16_ok((const uint8_t *)words, fi.frame_off, end_byte + 2u)) ok = false;
+    if (ok && !(ablate & 1u) && !st_crc16_frame((const uint8_t *)words, crcp, f, fi.frame_off, end_byte + 2u)) ok = false;
     if (ok && crc != crc_read) ok = false;
     if (ok) {
         info[f].resume_bit = resume;
@@ -4553,23 +4664,23 @@ hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
 /* stereo fast path; launched before k_decode<8> (it hands frames back to it) */
 hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                     uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                                    const uint32_t *perm, uint32_t mode, hipStream_t s) {
+                                    const uint32_t *perm, uint32_t mode, const uint32_t *crcp, hipStream_t s) {
     const dim3 grid((nframes + 63) / 64);
     const uint32_t ab = ablate_flags() | mode;
     if (ab & 0x400u) return hipSuccess; /* timing ablation: everything to k_decode<8> */
 #if BNF_TU == 3
     (void)fmt;
-    hipLaunchKernelGGL(k_decode_st<BNF_OUT_FLACDECODER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+    hipLaunchKernelGGL(k_decode_st<BNF_OUT_FLACDECODER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab, crcp);
 #else
     switch (fmt) {
     case BNF_OUT_PLANAR32:
-        hipLaunchKernelGGL(k_decode_st<BNF_OUT_PLANAR32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_PLANAR32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab, crcp);
         break;
     case BNF_OUT_INTERLEAVED32:
-        hipLaunchKernelGGL(k_decode_st<BNF_OUT_INTERLEAVED32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_INTERLEAVED32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab, crcp);
         break;
     default:
-        hipLaunchKernelGGL(k_decode_st<BNF_OUT_FILEREADER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        hipLaunchKernelGGL(k_decode_st<BNF_OUT_FILEREADER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab, crcp);
         break;
     }
 #endif
@@ -4598,18 +4709,18 @@ hipError_t TU_FN(bnf_stats)(uint64_t *out16, int reset) {
 /* stereo frames above 16 bits; launched before k_decode<8>/<16>/<32> (it hands frames back to k_decode<16>) */
 hipError_t bnf_launch_decode_sw_tu7(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                                     uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                                    const uint32_t *perm, uint32_t mode, hipStream_t s) {
+                                    const uint32_t *perm, uint32_t mode, const uint32_t *crcp, hipStream_t s) {
     const dim3 grid((nframes + 63) / 64);
     const uint32_t ab = ablate_flags() | mode;
     switch (fmt) {
     case BNF_OUT_PLANAR32:
-        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_PLANAR32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_PLANAR32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab, crcp);
         break;
     case BNF_OUT_INTERLEAVED32:
-        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_INTERLEAVED32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_INTERLEAVED32>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab, crcp);
         break;
     case BNF_OUT_FILEREADER:
-        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_FILEREADER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab);
+        hipLaunchKernelGGL(k_decode_sw<BNF_OUT_FILEREADER>, grid, dim3(64), 0, s, words, nbytes, nframes, sp, chn_lanes, out, out_bytes, info, perm, ab, crcp);
         break;
     default: return hipErrorInvalidValue;
     }
@@ -4627,11 +4738,11 @@ void bnf_set_ablate_tu4(uint32_t);
 hipError_t bnf_stats_tu3(uint64_t *, int);
 hipError_t bnf_stats_tu4(uint64_t *, int);
 hipError_t bnf_launch_decode_tu3(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, const uint32_t *, hipStream_t);
 hipError_t bnf_launch_decode_tu4(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
+                                 uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, const uint32_t *, hipStream_t);
 hipError_t bnf_launch_decode_sw_tu7(const uint32_t *, uint64_t, uint32_t, bnf_stream_params, uint32_t, int, uint8_t *,
-                                    uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, hipStream_t);
+                                    uint64_t, bnf_frame_info *, const uint32_t *, uint32_t, const uint32_t *, hipStream_t);
 hipError_t bnf_upload_tables_tu5(const uint8_t *, const uint16_t *, const uint16_t *);
 void bnf_set_ablate_tu5(uint32_t);
 hipError_t bnf_stats_tu5(uint64_t *, int);
@@ -4902,7 +5013,23 @@ static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32
     return (uint64_t)nframes * chn_lanes < (uint64_t)lim * 64u;
 }
 
+/* The CRC-16 hand-off (crcp, CRCP_WORDS): 0 none (the decode tails read every frame again),
+ * 1 k_parse folds channel 0's lines from its ring while walking (the prefix), 2 and the rest of
+ * the span to the next frame at its end (the verdict).  Env BNFLAC_CRC_MODE; bnf_set_crc_mode. */
+static std::atomic<int> g_crc_mode{-1};
+static int crc_mode() {
+    int m = g_crc_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char *e = getenv("BNFLAC_CRC_MODE");
+        m = e ? std::min(std::max(atoi(e), 0), 2) : 1;
+        g_crc_mode.store(m, std::memory_order_relaxed);
+    }
+    return m;
+}
+
 extern "C" {
+int bnf_crc_mode() { return crc_mode(); }
+void bnf_set_crc_mode(int mode) { g_crc_mode.store(mode < 0 ? -1 : std::min(mode, 2), std::memory_order_relaxed); } /* -1: env */
 uint64_t bnf_decode_seg_launches() { return g_seg_launches.load(std::memory_order_relaxed); }
 void bnf_set_decode_sys(int mode) { g_decode_sys.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
 void bnf_set_parse_wave(int mode) { g_parse_wave.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
@@ -4916,9 +5043,13 @@ hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset) { /* debug counters o
 }
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
                             bnf_stream_params sp, const uint64_t *out_sample_in, uint64_t base_sample,
-                            bnf_frame_info *info, uint32_t *order, hipStream_t s) {
+                            bnf_frame_info *info, uint32_t *order, uint32_t *crcp, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
     if (use_parse_wave(nframes, sp)) {
+        if (crcp) { /* no prefix from the wave walk */
+            const hipError_t e = hipMemsetAsync(crcp, 0, 4ull * CRCP_WORDS * nframes, s);
+            if (e != hipSuccess) return e;
+        }
         static const uint32_t pws = getenv("BNFLAC_PW_STATS") ? 1u : 0u;
         static const int seg = [] { const char *e = getenv("BNFLAC_PW_SEG"); return e ? atoi(e) : 0; }();
         hipLaunchKernelGGL(k_parse_wave, dim3(nframes), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
@@ -4936,8 +5067,17 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
         hipError_t e = launch_order<1>(nullptr, (const uint8_t *)words, nbytes, frame_offs, nframes, order, &perm, s);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_parse, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
-                       out_sample_in, base_sample, info, ablate_flags(), perm);
+    /* the CRC-16 hand-off (crcp; crc_mode) */
+    const int cm = crcp ? crc_mode() : 0;
+    if (cm == 2)
+        hipLaunchKernelGGL(k_parse<2>, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
+                           out_sample_in, base_sample, info, ablate_flags(), perm, crcp);
+    else if (cm == 1)
+        hipLaunchKernelGGL(k_parse<1>, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
+                           out_sample_in, base_sample, info, ablate_flags(), perm, crcp);
+    else
+        hipLaunchKernelGGL(k_parse<0>, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
+                           out_sample_in, base_sample, info, ablate_flags(), perm, nullptr);
     return hipGetLastError();
 }
 
@@ -4952,7 +5092,7 @@ hipError_t bnf_launch_fill_bad(const bnf_frame_info *info, uint32_t nframes, bnf
 
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes, bnf_stream_params sp,
                              uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes, bnf_frame_info *info,
-                             uint32_t *order, hipStream_t s) {
+                             uint32_t *order, const uint32_t *crcp, hipStream_t s) {
     if (!nframes || !nbytes) return hipSuccess;
     uint32_t mode = 0;
     /* every frame through k_decode_sys (decode order by class and blocksize), then its
@@ -5019,13 +5159,13 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
     };
     if (sq && fm == 2 && e == hipSuccess) e = fork();
     if (sw) {
-        if (e == hipSuccess) e = bnf_launch_decode_sw_tu7(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+        if (e == hipSuccess) e = bnf_launch_decode_sw_tu7(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, crcp, s);
         mode |= BNF_MODE_SW;
     }
     if (e == hipSuccess)
         e = fmt == BNF_OUT_FLACDECODER
-                ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s)
-                : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, s);
+                ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, crcp, s)
+                : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, crcp, s);
     if (sq && fm == 1 && e == hipSuccess) e = fork();
     if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, nullptr, s);
     if (sq) {

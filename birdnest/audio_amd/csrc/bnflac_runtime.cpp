@@ -44,11 +44,13 @@ void bnf_set_ablate(uint32_t v);
 hipError_t bnf_stats(uint64_t *out16, int reset);
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs,
                             uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
-                            uint64_t base_sample, bnf_frame_info *info, uint32_t *order, hipStream_t s);
-/* order: nullptr, or 256 + nframes words of device scratch for the frame order (k_order_*) */
+                            uint64_t base_sample, bnf_frame_info *info, uint32_t *order, uint32_t *crcp,
+                            hipStream_t s);
+/* order: nullptr, or 256 + nframes words of device scratch for the frame order (k_order_*);
+ * crcp: nullptr, or k_parse's CRC-16 hand-off for these frames (8 words per frame) */
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes,
                              bnf_stream_params sp, uint32_t chn_lanes, int fmt, uint8_t *out, uint64_t out_bytes,
-                             bnf_frame_info *info, uint32_t *order, hipStream_t s);
+                             bnf_frame_info *info, uint32_t *order, const uint32_t *crcp, hipStream_t s);
 hipError_t bnf_launch_fill_bad(const bnf_frame_info *info, uint32_t nframes, bnf_stream_params sp, int fmt,
                                uint8_t *out, uint64_t out_bytes, hipStream_t s);
 hipError_t bnf_launch_chain(const uint8_t *bytes, uint64_t nbytes, const uint64_t *cand, uint32_t ncand,
@@ -142,6 +144,10 @@ extern "C" void bnf_set_decode_sys(int mode);
 /* k_decode_sys (systolic restore, every frame class): -1 auto (BNFLAC_DECODE_SYS), 0 the lane
  * kernels by class, 1 always (tests, A/B) */
 extern "C" BNFLAC_API void bnflac_debug_set_decode_sys(int mode) { bnf_set_decode_sys(mode); }
+extern "C" int bnf_crc_mode();
+extern "C" void bnf_set_crc_mode(int mode);
+/* the CRC-16 hand-off: -1 env BNFLAC_CRC_MODE (default 1), 0 none, 1 k_parse's prefix, 2 + its verdict */
+extern "C" BNFLAC_API void bnflac_debug_set_crc_mode(int mode) { bnf_set_crc_mode(mode); }
 extern "C" uint64_t bnf_decode_seg_launches();
 extern "C" BNFLAC_API uint64_t bnflac_debug_decode_seg_launches(void) { return bnf_decode_seg_launches(); }
 extern "C" hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset);
@@ -187,7 +193,17 @@ struct bnflac_ctx {
     /* bnflac_index_stream scratch */
     CtxBuf cand, info, gap, jump, mark, pos, bs, small;
     CtxBuf order, porder; /* decode / parse order: histogram + permutation (k_order_*) */
+    /* k_parse's CRC-16 hand-off of the last bnflac_parse_frames batch (8 words per frame), and
+     * the batch they belong to: bnflac_decode_parsed uses them only for that same batch */
+    CtxBuf crcp;
+    const void *crcp_bytes = nullptr, *crcp_info = nullptr;
+    uint64_t crcp_nbytes = 0;
+    uint32_t crcp_n = 0;
 };
+
+/* crc mode 0: no CRC-16 hand-off, the decode tails check the whole frame (1 / 2 choose who
+ * computes it: bnf_launch_parse) */
+static bool crc_prefix_on() { return bnf_crc_mode() != 0; }
 
 extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
     *out = nullptr;
@@ -198,11 +214,22 @@ extern "C" BNFLAC_API int bnflac_ctx_create(int device, bnflac_ctx **out) {
     return 0;
 }
 
+/* Debug: the CRC-16 hand-off of the ctx's last bnflac_parse_frames (8 words per frame, see
+ * CRCP_WORDS in bnflac_kernels.hip), synchronously; -1 when there is none for nframes frames */
+extern "C" BNFLAC_API int bnflac_debug_crc_handoff(bnflac_ctx *ctx, uint32_t *out, uint32_t nframes) {
+    if (!ctx || !out) return fail("bnflac_debug_crc_handoff: null argument");
+    if (!ctx->crcp_bytes || ctx->crcp_n != nframes) return fail("bnflac_debug_crc_handoff: no hand-off for this batch");
+    DevGuard dg(ctx->device);
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(out, ctx->crcp.p, 32ull * nframes, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail("bnflac_debug_crc_handoff: HIP error");
+    return 0;
+}
+
 extern "C" BNFLAC_API void bnflac_ctx_destroy(bnflac_ctx *ctx) {
     if (!ctx) return;
     if (ctx->d_block_counts) (void)hipFree(ctx->d_block_counts);
     for (CtxBuf *b : {&ctx->cand, &ctx->info, &ctx->gap, &ctx->jump, &ctx->mark, &ctx->pos, &ctx->bs, &ctx->small,
-                      &ctx->order, &ctx->porder})
+                      &ctx->order, &ctx->porder, &ctx->crcp})
         b->release();
     delete ctx;
 }
@@ -272,9 +299,17 @@ extern "C" BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_
     memcpy(&p, sp, sizeof p);
     if (!ctx->porder.grow(sizeof(uint32_t) * (256u + (size_t)nframes)))
         return fail("bnflac_parse_frames: out of device memory (parse-order scratch)");
+    ctx->crcp_bytes = ctx->crcp_info = nullptr; /* no prefixes until this launch is enqueued */
+    const bool pre = crc_prefix_on() && ctx->crcp.grow(32u * std::max<size_t>(nframes, 1u));
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, d_frame_offsets,
                                     nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info,
-                                    (uint32_t *)ctx->porder.p, (hipStream_t)hs);
+                                    (uint32_t *)ctx->porder.p, pre ? (uint32_t *)ctx->crcp.p : nullptr, (hipStream_t)hs);
+    if (e == hipSuccess && pre) {
+        ctx->crcp_bytes = d_bytes;
+        ctx->crcp_info = d_info;
+        ctx->crcp_nbytes = nbytes;
+        ctx->crcp_n = nframes;
+    }
     return e == hipSuccess ? 0 : fail(std::string("k_parse: ") + hipGetErrorString(e));
 }
 
@@ -289,9 +324,14 @@ extern "C" BNFLAC_API int bnflac_decode_parsed(bnflac_ctx *ctx, const uint8_t *d
     /* decode order (256 + nframes) + k_decode_sys's hand-back list (4 + nframes) */
     if (!ctx->order.grow(sizeof(uint32_t) * (260u + 2u * (size_t)nframes)))
         return fail("bnflac_decode_parsed: out of device memory (decode-order scratch)");
+    /* the parse of this same batch on this context handed over its CRC-16 work (used once) */
+    const bool pre = ctx->crcp_bytes == d_bytes && ctx->crcp_info == d_info && ctx->crcp_nbytes == nbytes &&
+                     ctx->crcp_n == nframes;
+    ctx->crcp_bytes = ctx->crcp_info = nullptr;
     hipError_t e = bnf_launch_decode((const uint32_t *)d_bytes, nbytes, nframes, p,
                                      lanes_for(sp->channels), out_format, d_out, out_bytes, (bnf_frame_info *)d_info,
-                                     (uint32_t *)ctx->order.p, (hipStream_t)hs);
+                                     (uint32_t *)ctx->order.p, pre ? (const uint32_t *)ctx->crcp.p : nullptr,
+                                     (hipStream_t)hs);
     if (e == hipSuccess) /* a non-OK frame's range: zeros (include/bnflac.h) */
         e = bnf_launch_fill_bad((const bnf_frame_info *)d_info, nframes, p, out_format, d_out, out_bytes, (hipStream_t)hs);
     return e == hipSuccess ? 0 : fail(std::string("k_decode: ") + hipGetErrorString(e));
@@ -339,9 +379,10 @@ extern "C" BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_
         return fail("bnflac_index_stream: out of device memory");
     bnf_stream_params p;
     memcpy(&p, sp, sizeof p);
+    ctx->crcp_bytes = ctx->crcp_info = nullptr; /* the records this writes carry no CRC-16 hand-off */
     /* 2. header, CRC-8 and subframe walk of every candidate */
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, p, nullptr,
-                                    0, (bnf_frame_info *)ctx->info.p, nullptr, s);
+                                    0, (bnf_frame_info *)ctx->info.p, nullptr, nullptr, s);
     /* 3. successor chain, EOS rule, compaction */
     if (e == hipSuccess)
         e = bnf_launch_chain(d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, (const bnf_frame_info *)ctx->info.p,
@@ -791,7 +832,7 @@ bool decode_window(Dec *d, uint64_t base) {
             }
             if (!d->d_info.grow(sizeof(bnf_frame_info) * ncand)) goto oom;
             if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, n, (const uint64_t *)d->d_cand.p, ncand, sp,
-                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, nullptr, d->stream) != hipSuccess)
+                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, nullptr, nullptr, d->stream) != hipSuccess)
                 goto hip_fail;
             if (hipMemcpyAsync(d->info.data(), d->d_info.p, sizeof(bnf_frame_info) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
                 goto hip_fail;
@@ -813,7 +854,7 @@ bool decode_window(Dec *d, uint64_t base) {
             spd.channels = pcm_ch;
             if (bnf_launch_decode((const uint32_t *)d->d_bytes.p, n, ncand, spd, lanes_for(pcm_ch), BNF_OUT_PLANAR32,
                                   (uint8_t *)d->d_pcm.p, (uint64_t)std::max<uint64_t>(tot, 1) * pcm_ch * 4,
-                                  (bnf_frame_info *)d->d_info.p, nullptr, d->stream) != hipSuccess)
+                                  (bnf_frame_info *)d->d_info.p, nullptr, nullptr, d->stream) != hipSuccess)
                 goto hip_fail;
             d->pcm.resize((size_t)tot * pcm_ch);
             if (tot && hipMemcpyAsync(d->pcm.data(), d->d_pcm.p, sizeof(int32_t) * (size_t)tot * pcm_ch, hipMemcpyDeviceToHost, d->stream) != hipSuccess)

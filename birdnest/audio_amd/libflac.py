@@ -125,7 +125,8 @@ DECODER_SYMBOLS = [
 BATCH_SYMBOLS = ["bnflac_ctx_create", "bnflac_ctx_destroy", "bnflac_last_error", "bnflac_device_count",
                  "bnflac_index_frames", "bnflac_decode_frames", "bnflac_parse_frames", "bnflac_decode_parsed",
                  "bnflac_out_stride", "bnflac_debug_set_ablate", "bnflac_debug_stats", "bnflac_debug_set_parse_wave", "bnflac_debug_parse_wave_stats",
-                 "bnflac_debug_set_decode_sys", "bnflac_debug_decode_seg_launches", "bnflac_md5_interleaved32", "bnflac_index_stream"]
+                 "bnflac_debug_set_decode_sys", "bnflac_debug_decode_seg_launches", "bnflac_md5_interleaved32", "bnflac_index_stream",
+                 "bnflac_debug_set_crc_mode", "bnflac_debug_crc_handoff"]
 READER_SYMBOLS = ["bnflac_reader_open", "bnflac_reader_params", "bnflac_reader_read", "bnflac_reader_close",
                   "bnflac_reader_last_error", "bnflac_reader_seek", "bnflac_reader_read_filereader",
                   "bnflac_reader_pool_release"]
@@ -176,6 +177,9 @@ def load() -> ctypes.CDLL:
     L.bnflac_debug_set_ablate.argtypes = [ctypes.c_uint32]
     L.bnflac_debug_set_parse_wave.argtypes = [ctypes.c_int]
     L.bnflac_debug_set_decode_sys.argtypes = [ctypes.c_int]
+    L.bnflac_debug_set_crc_mode.argtypes = [ctypes.c_int]
+    L.bnflac_debug_crc_handoff.restype = i
+    L.bnflac_debug_crc_handoff.argtypes = [p, p, ctypes.c_uint32]
     L.bnflac_debug_decode_seg_launches.restype, L.bnflac_debug_decode_seg_launches.argtypes = ctypes.c_uint64, []
     L.bnflac_debug_parse_wave_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.bnflac_debug_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
@@ -414,6 +418,13 @@ class BatchDecoder:
                                          self._stream(stream))
         if rc != 0:
             raise RuntimeError(self.L.bnflac_last_error().decode())
+
+    def crc_handoff(self, nframes: int) -> np.ndarray:
+        """Debug: the CRC-16 hand-off of the last parse_frames call, [nframes, 8] uint32."""
+        a = np.zeros(8 * nframes, np.uint32)
+        if self.L.bnflac_debug_crc_handoff(self.ctx, a.ctypes.data_as(ctypes.c_void_p), nframes) != 0:
+            raise RuntimeError(self.L.bnflac_last_error().decode())
+        return a.reshape(nframes, 8)
 
 
 class Reader:

@@ -168,7 +168,10 @@ BNFLAC_API int bnflac_decode_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uin
 /* The two phases of bnflac_decode_frames, for callers that time or overlap them:
  * parse = frame headers + subframe cursor walk (k_parse), decode = subframe decode,
  * decorrelation, packing and CRC-16 (k_decode).  decode must follow parse on the same
- * stream with the same arguments. */
+ * stream with the same arguments.  The parse also does part of the CRC-16 work of 2-channel
+ * frames and hands it to the next bnflac_decode_parsed call on the same ctx with the same
+ * d_bytes, nbytes, d_info and nframes (used once; bnflac_index_stream drops it): the frame
+ * bytes must not change between the two calls (bnflac_debug_set_crc_mode). */
 BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
                                    const uint64_t *d_frame_offsets, uint32_t nframes,
                                    const bnflac_stream_params *sp, const uint64_t *d_out_sample,
@@ -190,6 +193,15 @@ BNFLAC_API void bnflac_debug_set_parse_wave(int mode);
  * (-1 auto: env BNFLAC_DECODE_SYS, else k_decode_sys for launches below 1024 subframe waves of
  * the lane kernels; 0 the lane kernels by class; 1 always); identical PCM and records. */
 BNFLAC_API void bnflac_debug_set_decode_sys(int mode);
+/* Development / test switch: who computes the CRC-16 hand-off bnflac_parse_frames passes to
+ * bnflac_decode_parsed (-1 env BNFLAC_CRC_MODE, default 1; 0 none: the decode reads every frame
+ * again; 1 k_parse's prefix: the lines before channel 1; 2 and its verdict over the span to
+ * the next frame's offset); identical PCM and records. */
+BNFLAC_API void bnflac_debug_set_crc_mode(int mode);
+/* Debug: the hand-off of ctx's last bnflac_parse_frames call (8 words per frame: prefix
+ * remainder r0, r1 | parity << 31, its lines + 1, frame_off low word; span to the next
+ * offset, verdict over it, frame_off low word, 0), synchronously.  0, or -1 when none. */
+BNFLAC_API int bnflac_debug_crc_handoff(bnflac_ctx *ctx, uint32_t *out, uint32_t nframes);
 /* Debug: how many decodes of this process took the W16 / W32 classes through one small
  * segment grid (k_decode_seg: the previous decode order on the device had neither class)
  * instead of the two full-size side grids. */

@@ -292,8 +292,139 @@ def test_crc_mismatch_and_junk_gap(gpu):
                                   np.delete(s.pcm, np.s_[2 * bs: 3 * bs], axis=0)), cfg
 
 
+@pytest.fixture
+def crc_mode(request, gpu):
+    """Who computes the CRC-16 hand-off for one test (bnflac_debug_set_crc_mode), with the
+    lane-per-frame k_parse forced (small batches otherwise take k_parse_wave, which hands
+    nothing over); the defaults after."""
+    torch, libflac, _ = gpu
+    L = libflac.load()
+    L.bnflac_debug_set_crc_mode(request.param)
+    L.bnflac_debug_set_parse_wave(0)
+    yield request.param
+    L.bnflac_debug_set_parse_wave(-1)
+    L.bnflac_debug_set_crc_mode(-1)
+
+
+@LANE
+@pytest.mark.parametrize("crc_mode", [0, 1, 2], indirect=True)
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_crc_handoff_paths(gpu, cfg, decode_mode, crc_mode):
+    """k_parse's CRC-16 hand-off to the stereo decode tails (include/bnflac.h), on each of its
+    paths, with damage past the part k_parse folds while walking channel 0: a frame that ends
+    at the next frame's offset (k_parse's verdict), one followed by junk and the batch's last
+    frame (its prefix continued by the tail).  A second decode of the same parsed records has
+    no hand-off (the whole frame again) and must give the same records and PCM."""
+    from birdnest.audio_amd import synth
+    torch, libflac, dec = gpu
+    s = synth.encode(synth.config(cfg, nframes=8, last_blocksize=0))
+    d = bytearray(s.data.tobytes())
+    o = [int(x) for x in s.frame_offsets]
+    ends = o[1:] + [len(d)]
+    d[ends[3] - 1] ^= 0x01                       # frame 3: its footer (verdict path)
+    d[ends[5] - 40] ^= 0x08                      # frame 5: channel 1's bytes, junk after it
+    d[ends[7] - 40] ^= 0x08                      # frame 7, the last: channel 1's bytes
+    junk = bytes([0x5A, 0x00, 0x13] * 7)
+    d = d[: o[6]] + junk + d[o[6]:]
+    o = o[:6] + [x + len(junk) for x in o[6:]]
+    fmt = libflac.OUT_INTERLEAVED32
+    sp = _stream_params(libflac, bytes(d))
+    dev = torch.device("cuda:0")
+    n = len(d)
+    d_bytes = torch.zeros((n + 15) // 16 * 16 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:n] = torch.frombuffer(bytearray(d), dtype=torch.uint8).to(dev)
+    offs = torch.tensor(o, dtype=torch.int64, device=dev)
+    stride = libflac.out_stride(fmt, sp)
+    outs, infos = [], []
+    d_info = torch.zeros(len(o) * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    dec.parse_frames(d_bytes, n, offs, len(o), sp, d_info)
+    parsed = d_info.clone()
+    for _ in range(2):
+        d_info.copy_(parsed)
+        d_out = torch.full((sp.total_samples * stride + 64,), 0xAB, dtype=torch.uint8, device=dev)
+        dec.decode_parsed(d_bytes, n, len(o), sp, fmt, d_out, d_info)
+        torch.cuda.synchronize()
+        outs.append(d_out[: sp.total_samples * stride].cpu().numpy())
+        infos.append(libflac.info_array(d_info.cpu().numpy()))
+    for info in infos:
+        good = (info["status"] == 0) & (info["crc_ok"] == 1)
+        assert good.tolist() == [True, True, True, False, True, False, True, False], cfg
+        assert info["crc_ok"][3] == 0 and info["status"][3] == 0, cfg
+    assert np.array_equal(outs[0], outs[1]), cfg
+    assert np.array_equal(infos[0], infos[1]), cfg
+    pcm = outs[0].view("<i4").reshape(-1, s.pcm.shape[1])
+    bs = s.params.blocksize
+    keep = np.ones(len(pcm), bool)
+    for f in (3, 5, 7):
+        keep[f * bs:(f + 1) * bs] = False
+        if infos[0]["status"][f] == 0:
+            assert not pcm[f * bs:(f + 1) * bs].any(), (cfg, f)
+    assert np.array_equal(pcm[keep], s.pcm[keep]), cfg
+
+
+_T15 = (1 << 15) | 3  # T = x^15 + x + 1: P = (x + 1) T (the tails' zero test, bnflac_kernels.hip)
+
+
+def _gf2_mod(a: int, m: int) -> int:
+    dm = m.bit_length() - 1
+    while a and a.bit_length() - 1 >= dm:
+        a ^= m << (a.bit_length() - 1 - dm)
+    return a
+
+
+@pytest.mark.parametrize("crc_mode", [1, 2], indirect=True)
+def test_crc_handoff_against_oracle(gpu, crc_mode):
+    """The hand-off itself (bnflac_debug_crc_handoff) against the oracle: each prefix holds the
+    remainder mod T and the parity of the frame's whole lines before channel 1, and each
+    verdict (mode 2) is the zero test of the CRC-16 over [offset, next offset) (frame + footer,
+    or + junk)."""
+    import oracle
+    from birdnest.audio_amd import synth
+    torch, libflac, dec = gpu
+    s = synth.encode(synth.config("C2", nframes=10, last_blocksize=0, seed=13))
+    d = bytearray(s.data.tobytes())
+    o = [int(x) for x in s.frame_offsets]
+    d[o[2] + 100] ^= 0x40
+    d[o[4 + 1] - 30] ^= 0x02
+    junk = bytes([0x77, 0x01] * 9)
+    d = d[: o[7]] + junk + d[o[7]:]
+    o = o[:7] + [x + len(junk) for x in o[7:]]
+    d = bytes(d)
+    sp = _stream_params(libflac, d)
+    dev = torch.device("cuda:0")
+    n = len(d)
+    d_bytes = torch.zeros((n + 15) // 16 * 16 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:n] = torch.frombuffer(bytearray(d), dtype=torch.uint8).to(dev)
+    nf = len(o)
+    d_info = torch.zeros(nf * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    dec.parse_frames(d_bytes, n, torch.tensor(o, dtype=torch.int64, device=dev), nf, sp, d_info)
+    h = dec.crc_handoff(nf).astype(np.int64)
+    spans = prefixes = 0
+    for f in range(nf):
+        if h[f, 4]:
+            assert crc_mode == 2, f
+            nx = o[f + 1]
+            assert h[f, 4] == nx - o[f] and h[f, 6] == o[f] & 0xFFFFFFFF, f
+            assert h[f, 5] == int(oracle.crc16(d[o[f]:nx]) == 0), f
+            spans += 1
+        if h[f, 2]:
+            assert h[f, 3] == o[f] & 0xFFFFFFFF, f
+            end = ((o[f] >> 6) + int(h[f, 2]) - 1) * 64
+            m = int.from_bytes(d[o[f]:end], "big")
+            r = ((int(h[f, 1]) & 0x0FFFFFFF) << 32) | int(h[f, 0])
+            assert _gf2_mod(r, _T15) == _gf2_mod(m, _T15), f
+            assert (int(h[f, 1]) >> 31) == bin(m).count("1") & 1, f
+            prefixes += 1
+    assert h[nf - 1, 4] == 0                    # the last frame: no next offset
+    # frame 2's damage may end k_parse's walk early (no hand-off for it)
+    assert prefixes >= nf - 1
+    if crc_mode == 2:
+        assert spans >= nf - 2 and h[2, 5] == 0
+        assert h[4, 4] and h[4, 5] == 0 and h[6, 4] and h[6, 5] == 0 and h[0, 4] and h[0, 5] == 1
+
+
 # ---------------------------------------------------------- libFLAC API parity
-STREAM_CASES = [k for k, v in GOLD.items() if v["kind"] in ("roundtrip", "error", "rfc")]
+STREAM_CASES =[k for k, v in GOLD.items() if v["kind"] in ("roundtrip", "error", "rfc")]
 
 
 @pytest.mark.parametrize("name", STREAM_CASES)
