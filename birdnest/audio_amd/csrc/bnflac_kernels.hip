@@ -812,11 +812,14 @@ DEV void crcp_fold(CrcP &c, const u32x4 (&v)[4]) {
     for (uint32_t i = 0; i < 4; i++) crcz_blk(c.z, make_uint4(v[i].x, v[i].y, v[i].z, v[i].w));
     c.wc++;
 }
-/* fold the lines wholly before the cursor (whole wave; the ring's two lines are
- * [iend / 4 - 2, iend / 4), landed once behind the cursor).  The frame's first line is folded
- * before the walk (parse_frame), so these are whole lines. */
-DEV void crcp_hook(CrcP &c, const BR &b, uint32_t lane) {
-    const uint32_t cl = (uint32_t)(br_pos(b) >> 9);
+/* fold the lines before line cl (whole wave).  The ring holds the two lines [iend / 4 - 2,
+ * iend / 4), and the refill keeps the line of word wi (the reader's next word) and the one
+ * after it: so before a refill, cl = wi / 16 -- every line the reader has loaded, which the
+ * refill may overwrite -- folds from the ring (a line behind a landing refill reads again
+ * from global memory, L2-warm; bounding by the cursor's bit position instead left 22% of C2's
+ * lines to that path: the word lookahead crosses a line first).  The frame's first line is
+ * folded before the walk (parse_frame), so these are whole lines. */
+DEV void crcp_hook(CrcP &c, const BR &b, uint32_t lane, uint32_t cl) {
     while (any_lane(c.wc < cl)) {
         if (c.wc < cl) {
             const uint32_t L = c.wc;
@@ -1037,14 +1040,14 @@ DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit
     while (any_lane(rem != 0u || p < parts)) {
         if (BULK) {
             if (__builtin_amdgcn_readfirstlane(since) >= 12u && !(ablate & 32u)) { /* every 12-14 steps */
-                if (CP) crcp_hook(cp, b, lane); /* the lines behind the cursor, before the refill overwrites them */
+                if (CP) crcp_hook(cp, b, lane, b.wi >> 4); /* the lines loaded, before the refill overwrites them */
                 br_refill(b);
                 pk_resync(b, lane);
                 since = 0;
             }
             since += 2u;
         } else if ((__builtin_amdgcn_readfirstlane(since++) & 7u) == 0u && !(ablate & 32u)) { /* every 16 steps */
-            if (CP) crcp_hook(cp, b, lane);
+            if (CP) crcp_hook(cp, b, lane, b.wi >> 4);
             br_refill(b);
             pk_resync(b, lane);
         }
@@ -1738,16 +1741,16 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
     if (CPM && crcp) { /* the hand-off (CRCP_WORDS) to the k_decode_st / k_decode_sw tails */
         u32x4 o = u32x4{0u, 0u, 0u, 0u}, o2 = u32x4{0u, 0u, 0u, 0u};
         const uint32_t l1 = (uint32_t)(br_pos(b) >> 9); /* subframe 1's line */
-        if (cp.wc != ~0u && cp.wc <= l1 && st == BNF_ST_OK) {
-            crcp_hook(cp, b, threadIdx.x & 63u); /* every line before subframe 1's line */
+        if (cp.wc != ~0u && st == BNF_ST_OK) {
+            crcp_hook(cp, b, threadIdx.x & 63u, l1); /* every line before subframe 1's line (or more) */
             o = u32x4{cp.z.r0, (cp.z.r1 & 0x0FFFFFFFu) | ((uint32_t)(__builtin_popcount(cp.z.px) & 1) << 31),
                       cp.wc - (uint32_t)(fi.frame_off >> 6) + 1u, (uint32_t)fi.frame_off};
             /* the rest up to the next frame's offset: where a frame of a contiguous batch ends
              * (frame + footer), so its tail need not read the frame again */
             const uint64_t nx = CPM == 2 && f + 1u < nframes ? frame_offs[f + 1u] : 0u;
-            if (CPM == 2 && nx > (uint64_t)l1 * 64u && nx <= nbytes && nx - fi.frame_off < (1u << 24))
+            if (CPM == 2 && nx >= (uint64_t)cp.wc * 64u && nx <= nbytes && nx - fi.frame_off < (1u << 24))
                 o2 = u32x4{(uint32_t)(nx - fi.frame_off),
-                           st_crc16_ok<2>((const uint8_t *)words, fi.frame_off, nx, cp.z, (uint64_t)l1 * 64u) ? 1u : 0u,
+                           st_crc16_ok<2>((const uint8_t *)words, fi.frame_off, nx, cp.z, (uint64_t)cp.wc * 64u) ? 1u : 0u,
                            (uint32_t)fi.frame_off, 0u};
         }
         *(u32x4 *)(crcp + CRCP_WORDS * (uint64_t)f) = o;
