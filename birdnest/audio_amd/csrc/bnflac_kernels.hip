@@ -4890,6 +4890,7 @@ __global__ void __launch_bounds__(ORDER_NB) k_order_scan(uint32_t *__restrict__ 
     if (cls && i == ORDER_NB - 1u) {
         cls[0] = t[3u * 64u - 1u] - t[2u * 64u - 1u];
         cls[1] = t[4u * 64u - 1u] - t[3u * 64u - 1u];
+        cls[2] = t[ORDER_NB - 1u]; /* every frame of the order */
     }
 }
 template <int MODE>
@@ -4933,7 +4934,7 @@ static hipError_t launch_order(const bnf_frame_info *info, const uint8_t *bytes,
 struct SideQ {
     hipStream_t st[2]; /* W16, W32 */
     hipEvent_t fork, join[2];
-    uint32_t *cls; /* host memory: the last decode order's W16 / W32 class sizes (k_order_scan) */
+    uint32_t *cls; /* host memory: the last decode order's W16 / W32 class sizes and its frame count (k_order_scan) */
 };
 static std::mutex g_side_mu;
 static std::atomic<uint64_t> g_seg_launches{0}; /* k_decode_seg launches (bnf_decode_seg_launches) */
@@ -4958,7 +4959,7 @@ static SideQ *side_queue() { /* under g_side_mu; nullptr: decode serially */
             ok = hipStreamCreateWithFlags(&n.st[i], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&n.join[i], hipEventDisableTiming) == hipSuccess;
         if (ok && hipHostMalloc((void **)&n.cls, 64, hipHostMallocCoherent) != hipSuccess) n.cls = nullptr;
-        if (n.cls) n.cls[0] = n.cls[1] = ~0u; /* unknown: the full grids */
+        if (n.cls) n.cls[0] = n.cls[1] = n.cls[2] = ~0u; /* unknown: the full grids */
         if (!ok) {
             for (int i = 0; i < 2; i++) {
                 if (n.join[i]) (void)hipEventDestroy(n.join[i]);
@@ -5018,13 +5019,14 @@ static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32
 
 /* The CRC-16 hand-off (crcp, CRCP_WORDS): 0 none (the decode tails read every frame again),
  * 1 k_parse folds channel 0's lines from its ring while walking (the prefix), 2 and the rest of
- * the span to the next frame at its end (the verdict).  Env BNFLAC_CRC_MODE; bnf_set_crc_mode. */
+ * the span to the next frame at its end (the verdict), 3 (default) 1 where it pays (below).
+ * Env BNFLAC_CRC_MODE; bnf_set_crc_mode. */
 static std::atomic<int> g_crc_mode{-1};
 static int crc_mode() {
     int m = g_crc_mode.load(std::memory_order_relaxed);
     if (m < 0) {
         const char *e = getenv("BNFLAC_CRC_MODE");
-        m = e ? std::min(std::max(atoi(e), 0), 2) : 1;
+        m = e ? std::min(std::max(atoi(e), 0), 3) : 3;
         g_crc_mode.store(m, std::memory_order_relaxed);
     }
     return m;
@@ -5032,7 +5034,7 @@ static int crc_mode() {
 
 extern "C" {
 int bnf_crc_mode() { return crc_mode(); }
-void bnf_set_crc_mode(int mode) { g_crc_mode.store(mode < 0 ? -1 : std::min(mode, 2), std::memory_order_relaxed); } /* -1: env */
+void bnf_set_crc_mode(int mode) { g_crc_mode.store(mode < 0 ? -1 : std::min(mode, 3), std::memory_order_relaxed); } /* -1: env */
 uint64_t bnf_decode_seg_launches() { return g_seg_launches.load(std::memory_order_relaxed); }
 void bnf_set_decode_sys(int mode) { g_decode_sys.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
 void bnf_set_parse_wave(int mode) { g_parse_wave.store(mode < 0 ? 2 : (mode ? 1 : 0), std::memory_order_relaxed); } /* -1: auto */
@@ -5046,13 +5048,10 @@ hipError_t bnf_parse_wave_stats(uint64_t *out8, int reset) { /* debug counters o
 }
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs, uint32_t nframes,
                             bnf_stream_params sp, const uint64_t *out_sample_in, uint64_t base_sample,
-                            bnf_frame_info *info, uint32_t *order, uint32_t *crcp, hipStream_t s) {
+                            bnf_frame_info *info, uint32_t *order, uint32_t *crcp, bool *handed, hipStream_t s) {
+    if (handed) *handed = false;
     if (!nframes || !nbytes) return hipSuccess;
-    if (use_parse_wave(nframes, sp)) {
-        if (crcp) { /* no prefix from the wave walk */
-            const hipError_t e = hipMemsetAsync(crcp, 0, 4ull * CRCP_WORDS * nframes, s);
-            if (e != hipSuccess) return e;
-        }
+    if (use_parse_wave(nframes, sp)) { /* no CRC-16 hand-off from the wave walk */
         static const uint32_t pws = getenv("BNFLAC_PW_STATS") ? 1u : 0u;
         static const int seg = [] { const char *e = getenv("BNFLAC_PW_SEG"); return e ? atoi(e) : 0; }();
         hipLaunchKernelGGL(k_parse_wave, dim3(nframes), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
@@ -5070,8 +5069,23 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
         hipError_t e = launch_order<1>(nullptr, (const uint8_t *)words, nbytes, frame_offs, nframes, order, &perm, s);
         if (e != hipSuccess) return e;
     }
-    /* the CRC-16 hand-off (crcp; crc_mode) */
-    const int cm = crcp ? crc_mode() : 0;
+    /* the CRC-16 hand-off (crcp; crc_mode).  It only pays where the stereo decode tails are on
+     * the launch's critical path: not for a 16-bit stream whose previous decode order on this
+     * device (one batch behind, as for the segment grid) had a quarter or more W16 / W32
+     * frames, whose side instances then outlast k_decode_st (C4: k_parse +0.6 ms for no
+     * decode gain) */
+    int cm = crcp ? crc_mode() : 0;
+    if (cm == 3 && sp.bps <= 16u) {
+        std::lock_guard<std::mutex> lk(g_side_mu);
+        const SideQ *sq = side_queue();
+        if (sq && sq->cls) {
+            const uint32_t w16 = __atomic_load_n(&sq->cls[0], __ATOMIC_RELAXED), w32 = __atomic_load_n(&sq->cls[1], __ATOMIC_RELAXED),
+                           n = __atomic_load_n(&sq->cls[2], __ATOMIC_RELAXED);
+            if (w16 != ~0u && w32 != ~0u && n != ~0u && 4ull * ((uint64_t)w16 + w32) >= n && n) cm = 0;
+        }
+    }
+    if (cm == 3) cm = 1;
+    if (handed) *handed = cm != 0;
     if (cm == 2)
         hipLaunchKernelGGL(k_parse<2>, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
                            out_sample_in, base_sample, info, ablate_flags(), perm, crcp);

@@ -45,7 +45,7 @@ hipError_t bnf_stats(uint64_t *out16, int reset);
 hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64_t *frame_offs,
                             uint32_t nframes, bnf_stream_params sp, const uint64_t *out_sample_in,
                             uint64_t base_sample, bnf_frame_info *info, uint32_t *order, uint32_t *crcp,
-                            hipStream_t s);
+                            bool *handed, hipStream_t s);
 /* order: nullptr, or 256 + nframes words of device scratch for the frame order (k_order_*);
  * crcp: nullptr, or k_parse's CRC-16 hand-off for these frames (8 words per frame) */
 hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nframes,
@@ -146,7 +146,8 @@ extern "C" void bnf_set_decode_sys(int mode);
 extern "C" BNFLAC_API void bnflac_debug_set_decode_sys(int mode) { bnf_set_decode_sys(mode); }
 extern "C" int bnf_crc_mode();
 extern "C" void bnf_set_crc_mode(int mode);
-/* the CRC-16 hand-off: -1 env BNFLAC_CRC_MODE (default 1), 0 none, 1 k_parse's prefix, 2 + its verdict */
+/* the CRC-16 hand-off: -1 env BNFLAC_CRC_MODE (default 3), 0 none, 1 k_parse's prefix, 2 + its verdict,
+ * 3 the prefix where it pays (bnf_launch_parse) */
 extern "C" BNFLAC_API void bnflac_debug_set_crc_mode(int mode) { bnf_set_crc_mode(mode); }
 extern "C" uint64_t bnf_decode_seg_launches();
 extern "C" BNFLAC_API uint64_t bnflac_debug_decode_seg_launches(void) { return bnf_decode_seg_launches(); }
@@ -301,10 +302,12 @@ extern "C" BNFLAC_API int bnflac_parse_frames(bnflac_ctx *ctx, const uint8_t *d_
         return fail("bnflac_parse_frames: out of device memory (parse-order scratch)");
     ctx->crcp_bytes = ctx->crcp_info = nullptr; /* no prefixes until this launch is enqueued */
     const bool pre = crc_prefix_on() && ctx->crcp.grow(32u * std::max<size_t>(nframes, 1u));
+    bool handed = false;
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, d_frame_offsets,
                                     nframes, p, d_out_sample, base_sample, (bnf_frame_info *)d_info,
-                                    (uint32_t *)ctx->porder.p, pre ? (uint32_t *)ctx->crcp.p : nullptr, (hipStream_t)hs);
-    if (e == hipSuccess && pre) {
+                                    (uint32_t *)ctx->porder.p, pre ? (uint32_t *)ctx->crcp.p : nullptr, &handed,
+                                    (hipStream_t)hs);
+    if (e == hipSuccess && pre && handed) {
         ctx->crcp_bytes = d_bytes;
         ctx->crcp_info = d_info;
         ctx->crcp_nbytes = nbytes;
@@ -382,7 +385,7 @@ extern "C" BNFLAC_API int bnflac_index_stream(bnflac_ctx *ctx, const uint8_t *d_
     ctx->crcp_bytes = ctx->crcp_info = nullptr; /* the records this writes carry no CRC-16 hand-off */
     /* 2. header, CRC-8 and subframe walk of every candidate */
     hipError_t e = bnf_launch_parse((const uint32_t *)d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, p, nullptr,
-                                    0, (bnf_frame_info *)ctx->info.p, nullptr, nullptr, s);
+                                    0, (bnf_frame_info *)ctx->info.p, nullptr, nullptr, nullptr, s);
     /* 3. successor chain, EOS rule, compaction */
     if (e == hipSuccess)
         e = bnf_launch_chain(d_bytes, nbytes, (const uint64_t *)ctx->cand.p, ncand, (const bnf_frame_info *)ctx->info.p,
@@ -832,7 +835,7 @@ bool decode_window(Dec *d, uint64_t base) {
             }
             if (!d->d_info.grow(sizeof(bnf_frame_info) * ncand)) goto oom;
             if (bnf_launch_parse((const uint32_t *)d->d_bytes.p, n, (const uint64_t *)d->d_cand.p, ncand, sp,
-                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, nullptr, nullptr, d->stream) != hipSuccess)
+                                 nullptr, 0, (bnf_frame_info *)d->d_info.p, nullptr, nullptr, nullptr, d->stream) != hipSuccess)
                 goto hip_fail;
             if (hipMemcpyAsync(d->info.data(), d->d_info.p, sizeof(bnf_frame_info) * ncand, hipMemcpyDeviceToHost, d->stream) != hipSuccess)
                 goto hip_fail;

@@ -194,9 +194,10 @@ BNFLAC_API void bnflac_debug_set_parse_wave(int mode);
  * the lane kernels; 0 the lane kernels by class; 1 always); identical PCM and records. */
 BNFLAC_API void bnflac_debug_set_decode_sys(int mode);
 /* Development / test switch: who computes the CRC-16 hand-off bnflac_parse_frames passes to
- * bnflac_decode_parsed (-1 env BNFLAC_CRC_MODE, default 1; 0 none: the decode reads every frame
+ * bnflac_decode_parsed (-1 env BNFLAC_CRC_MODE, default 3; 0 none: the decode reads every frame
  * again; 1 k_parse's prefix: the lines before channel 1; 2 and its verdict over the span to
- * the next frame's offset); identical PCM and records. */
+ * the next frame's offset; 3 the prefix, except for a 16-bit stream after a decode on the
+ * device whose frames were a quarter or more LPC above order 8); identical PCM and records. */
 BNFLAC_API void bnflac_debug_set_crc_mode(int mode);
 /* Debug: the hand-off of ctx's last bnflac_parse_frames call (8 words per frame: prefix
  * remainder r0, r1 | parity << 31, its lines + 1, frame_off low word; span to the next
