@@ -362,6 +362,61 @@ def test_crc_handoff_paths(gpu, cfg, decode_mode, crc_mode):
     assert np.array_equal(pcm[keep], s.pcm[keep]), cfg
 
 
+@LANE
+@pytest.mark.parametrize("crc_mode", [1], indirect=True)
+def test_crc_handoff_contract(gpu, decode_mode, crc_mode):
+    """The hand-off's contract (include/bnflac.h): it belongs to the context's last
+    bnflac_parse_frames batch and the next decode takes it (used or not: a decode of other
+    records gets none and checks whole frames); bnflac_index_stream drops it.  Every path
+    decodes the same records."""
+    from birdnest.audio_amd import synth
+    torch, libflac, dec = gpu
+    s = synth.encode(synth.config("C2", nframes=12, last_blocksize=0, seed=17))
+    d = bytes(s.data.tobytes())
+    o = [int(x) for x in s.frame_offsets]
+    fmt = libflac.OUT_FLACDECODER
+    sp = _stream_params(libflac, d)
+    dev = torch.device("cuda:0")
+    n = len(d)
+    d_bytes = torch.zeros((n + 15) // 16 * 16 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:n] = torch.frombuffer(bytearray(d), dtype=torch.uint8).to(dev)
+    offs = torch.tensor(o, dtype=torch.int64, device=dev)
+    nf = len(o)
+    stride = libflac.out_stride(fmt, sp)
+    want = s.pcm.astype("<i2").tobytes()
+
+    def decode(d_info):
+        d_out = torch.zeros(sp.total_samples * stride, dtype=torch.uint8, device=dev)
+        dec.decode_parsed(d_bytes, n, nf, sp, fmt, d_out, d_info)
+        torch.cuda.synchronize()
+        info = libflac.info_array(d_info.cpu().numpy())
+        assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+        assert d_out.cpu().numpy().tobytes() == want
+        return info
+
+    d_info = torch.zeros(nf * libflac.FRAME_INFO_BYTES, dtype=torch.uint8, device=dev)
+    dec.parse_frames(d_bytes, n, offs, nf, sp, d_info)
+    h = dec.crc_handoff(nf)
+    assert (h[:, 2] != 0).sum() >= nf - 1          # prefixes were handed over
+    ref = decode(d_info)                              # ... and used
+    with pytest.raises(RuntimeError):                 # used once
+        dec.crc_handoff(nf)
+    # another records buffer than the parse wrote: no hand-off, same result, and the pending
+    # one is gone
+    dec.parse_frames(d_bytes, n, offs, nf, sp, d_info)
+    other = d_info.clone()
+    assert np.array_equal(decode(other), ref)
+    with pytest.raises(RuntimeError):
+        dec.crc_handoff(nf)
+    # bnflac_index_stream on the context drops it
+    dec.parse_frames(d_bytes, n, offs, nf, sp, d_info)
+    dec.crc_handoff(nf)
+    dec.index_stream(d_bytes, n, o[0], sp, nf + 16)
+    with pytest.raises(RuntimeError):
+        dec.crc_handoff(nf)
+    assert np.array_equal(decode(d_info), ref)
+
+
 _T15 = (1 << 15) | 3  # T = x^15 + x + 1: P = (x + 1) T (the tails' zero test, bnflac_kernels.hip)
 
 
