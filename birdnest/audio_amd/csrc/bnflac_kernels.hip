@@ -803,15 +803,66 @@ DEV void crcz_blk(CrcZ &c, uint4 v) {
  * one 16-byte block at a time (three live state words: k_parse's occupancy is LDS-bound at 5
  * waves per SIMD, ~100 VGPRs), and the decode tail continues from there, re-reading only the
  * rest of the frame. */
-struct CrcP {
-    CrcZ z;      /* remainder mod T^4 and parity of lines [frame_off / 64, wc) */
-    uint32_t wc; /* next line to fold (absolute 64-byte line index); ~0: no prefix for this frame */
+/* The prefix state, two forms (k_parse<CPM, Y>):
+ *  - Y (16-bit streams): the remainder mod Q(y) = y^15 + y + 1, y = x^32, in 15 words.
+ *    Q(y) = T(x^32) = T(x)^32 is a multiple of T, so it keeps M mod T; with whole words as
+ *    the coefficients a 64-byte line is 18 word XORs at once (S y^16 + sum W[i] y^(15-i):
+ *    y^15 = y + 1, y^16 = y^2 + y; checked against bit-serial division mod T in Python while
+ *    writing this) against 96 VALU through the T^4 form, and the words are taken as loaded
+ *    (little-endian): a byte swap permutes the bits of every word alike, so it is applied to
+ *    the 15 state words once, at the hand-off (crcp_z).  The state costs k_parse 128 VGPRs (4
+ *    waves per SIMD): C2's bulk walk gains (k_parse 2.52 -> 2.16 ms against 1.95 without the
+ *    prefix), while C3's plain walk lost with it (1.68 -> 2.18 ms on a build at 146 VGPRs,
+ *    3 waves), hence
+ *  - !Y (above 16 bits): the T^4 form of the decode tails (CrcZ, 3 words; 94 VGPRs, 5 waves). */
+template <bool Y> struct CrcPT;
+template <> struct CrcPT<true> {
+    uint32_t s[15]; /* s[k]: the coefficient of y^k (little-endian words) */
+    uint32_t px;    /* XOR of every word (parity) */
+    uint32_t wc;    /* next line to fold (absolute 64-byte line index); ~0: no prefix for this frame */
 };
-DEV void crcp_fold(CrcP &c, const u32x4 (&v)[4]) {
+template <> struct CrcPT<false> {
+    CrcZ z;      /* remainder mod T^4 and parity */
+    uint32_t wc;
+};
+DEV void crcp_init(CrcPT<true> &c) {
+#pragma unroll
+    for (int k = 0; k < 15; k++) c.s[k] = 0u;
+    c.px = 0u;
+    c.wc = ~0u;
+}
+DEV void crcp_init(CrcPT<false> &c) {
+    c.z = CrcZ{0u, 0u, 0u};
+    c.wc = ~0u;
+}
+DEV void crcp_fold(CrcPT<true> &c, const u32x4 (&v)[4]) {
+    const uint32_t W[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                            v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+    c.px ^= W[0] ^ W[1] ^ W[2] ^ W[3] ^ W[4] ^ W[5] ^ W[6] ^ W[7] ^ W[8] ^ W[9] ^ W[10] ^ W[11] ^ W[12] ^ W[13] ^
+            W[14] ^ W[15];
+    const uint32_t r0 = c.s[13] ^ c.s[14] ^ W[15] ^ W[0], r1 = c.s[0] ^ c.s[13] ^ W[14] ^ W[0],
+                   r2 = c.s[0] ^ c.s[1] ^ c.s[14] ^ W[13];
+#pragma unroll
+    for (int d = 14; d >= 3; d--) c.s[d] = c.s[d - 2] ^ c.s[d - 1] ^ W[15 - d]; /* descending: old s[d-2], s[d-1] */
+    c.s[2] = r2;
+    c.s[1] = r1;
+    c.s[0] = r0;
+    c.wc++;
+}
+DEV void crcp_fold(CrcPT<false> &c, const u32x4 (&v)[4]) {
 #pragma unroll
     for (uint32_t i = 0; i < 4; i++) crcz_blk(c.z, make_uint4(v[i].x, v[i].y, v[i].z, v[i].w));
     c.wc++;
 }
+/* the remainder in the decode tails' T^4 form (st_crc16_ok continues it) */
+DEV CrcZ crcp_z(const CrcPT<true> &c) {
+    CrcZ z{0u, 0u, 0u};
+#pragma unroll
+    for (int k = 14; k >= 0; k--) crcz_w(z, c.s[k]);
+    z.px = c.px;
+    return z;
+}
+DEV CrcZ crcp_z(const CrcPT<false> &c) { return c.z; }
 /* fold the lines before line cl (whole wave).  The ring holds the two lines [iend / 4 - 2,
  * iend / 4), and the refill keeps the line of word wi (the reader's next word) and the one
  * after it: so before a refill, cl = wi / 16 -- every line the reader has loaded, which the
@@ -819,8 +870,9 @@ DEV void crcp_fold(CrcP &c, const u32x4 (&v)[4]) {
  * from global memory, L2-warm; bounding by the cursor's bit position instead left 22% of C2's
  * lines to that path: the word lookahead crosses a line first).  The frame's first line is
  * folded before the walk (parse_frame), so these are whole lines. */
-DEV void crcp_hook(CrcP &c, const BR &b, uint32_t lane, uint32_t cl) {
-    while (any_lane(c.wc < cl)) {
+template <bool ALL = false, class C> /* ALL: every line before cl (the walk's end); else at most one (a refill point) */
+DEV void crcp_hook(C &c, const BR &b, uint32_t lane, uint32_t cl) {
+    for (uint32_t it = 0; any_lane(c.wc < cl) && (ALL || it == 0u); it++) {
         if (c.wc < cl) {
             const uint32_t L = c.wc;
             u32x4 v[4];
@@ -829,12 +881,13 @@ DEV void crcp_hook(CrcP &c, const BR &b, uint32_t lane, uint32_t cl) {
                 for (uint32_t i = 0; i < 4; i++)
                     v[i] = lds_ld128((const lds_u32x4 *)(b.ring + (((L & 1u) * 4u + i) * RING_LANE_DW) + lane * 4u));
                 lds_sync();
-            } else { /* overwritten by a refill: read it again */
+                crcp_fold(c, v);
+            } else { /* overwritten by a refill: read it again (each path folds: no merge of v) */
                 const u32x4 *g = (const u32x4 *)((const uint8_t *)b.w + (uint64_t)L * 64u);
 #pragma unroll
                 for (uint32_t i = 0; i < 4; i++) v[i] = g[i];
+                crcp_fold(c, v);
             }
-            crcp_fold(c, v);
         }
     }
 }
@@ -1028,8 +1081,8 @@ DEV void pkb_step(BR &b, uint32_t k1, uint32_t &nf, uint32_t laneb) {
 }
 /* BULK: with the bulk iterations (a separate instance: the plain loop keeps its registers);
  * CP: fold the CRC-16 prefix (crcp_hook) before each refill */
-template <bool BULK, bool CP>
-DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate, CrcP &cp) {
+template <bool BULK, bool CP, class C>
+DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate, C &cp) {
     const uint32_t parts = 1u << h.porder;
     const uint32_t psamples = h.porder ? bs >> h.porder : bs - h.order;
     const uint32_t plen = h.rice2 ? 5u : 4u, pesc = h.rice2 ? 31u : 15u;
@@ -1153,8 +1206,8 @@ DEV uint32_t skip_residual_t(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit
 /* The bulk instance when every lane's first partition has a small Rice parameter (k <= 9:
  * pairs of codewords fit a window; C2's k = 8), peeked at the cursor, which sits on that
  * parameter; the plain loop otherwise (C3 / C4: larger parameters, short partitions). */
-template <bool CP>
-DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate, CrcP &cp) {
+template <bool CP, class C>
+DEV uint32_t skip_residual(BR &b, const SubHdr &h, uint32_t bs, uint64_t limit, uint32_t ablate, C &cp) {
     const uint32_t k0 = br_peek(b) >> (h.rice2 ? 27u : 28u);
     if (!any_lane(k0 > 9u)) return skip_residual_t<true, CP>(b, h, bs, limit, ablate, cp);
     return skip_residual_t<false, CP>(b, h, bs, limit, ablate, cp);
@@ -1628,7 +1681,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 static_assert(PARSE_RD == 8, "pk_ra and the walk's pair steps (slot masks 0x3F3 / 0x1C0C, slot bits 10-12) assume an 8-slot ring");
 /* One lane per candidate frame: header + cursor walk over subframes 0..C-2.  Also
  * flags frames with an LPC order above 8 (they go to k_decode<32>). */
-template <int CPM> /* the CRC-16 hand-off (crc_mode): 1 the prefix, 2 the prefix and the verdict */
+template <int CPM, bool Y> /* the CRC-16 hand-off (crc_mode): 1 the prefix, 2 the prefix and the verdict; Y: its form (CrcPT) */
 DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const uint64_t *__restrict__ frame_offs,
                      uint32_t nframes, const bnf_stream_params &sp, const uint64_t *__restrict__ out_sample_in,
                      uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate, lds_u32 *ring,
@@ -1657,9 +1710,8 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
     const uint64_t fbit = fi.frame_off * 8u;
     BR b;
     br_init(b, words, nbytes, ring, threadIdx.x, PARSE_RD);
-    CrcP cp; /* the CRC-16 prefix of a 2-channel frame (crcp != nullptr: the batch decode's hand-off) */
-    cp.z = CrcZ{0u, 0u, 0u};
-    cp.wc = ~0u;
+    CrcPT<Y> cp; /* the CRC-16 prefix of a 2-channel frame (crcp != nullptr: the batch decode's hand-off) */
+    crcp_init(cp);
     uint32_t st = parse_header(b, fbit, limit, sp, fi);
     if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
     if (CPM && crcp != nullptr && st == BNF_ST_OK && fi.channels == 2u && !(ablate & 16u)) {
@@ -1742,15 +1794,16 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
         u32x4 o = u32x4{0u, 0u, 0u, 0u}, o2 = u32x4{0u, 0u, 0u, 0u};
         const uint32_t l1 = (uint32_t)(br_pos(b) >> 9); /* subframe 1's line */
         if (cp.wc != ~0u && st == BNF_ST_OK) {
-            crcp_hook(cp, b, threadIdx.x & 63u, l1); /* every line before subframe 1's line (or more) */
-            o = u32x4{cp.z.r0, (cp.z.r1 & 0x0FFFFFFFu) | ((uint32_t)(__builtin_popcount(cp.z.px) & 1) << 31),
+            crcp_hook<true>(cp, b, threadIdx.x & 63u, l1); /* every line before subframe 1's line (or more) */
+            const CrcZ z = crcp_z(cp);
+            o = u32x4{z.r0, (z.r1 & 0x0FFFFFFFu) | ((uint32_t)(__builtin_popcount(z.px) & 1) << 31),
                       cp.wc - (uint32_t)(fi.frame_off >> 6) + 1u, (uint32_t)fi.frame_off};
             /* the rest up to the next frame's offset: where a frame of a contiguous batch ends
              * (frame + footer), so its tail need not read the frame again */
             const uint64_t nx = CPM == 2 && f + 1u < nframes ? frame_offs[f + 1u] : 0u;
             if (CPM == 2 && nx >= (uint64_t)cp.wc * 64u && nx <= nbytes && nx - fi.frame_off < (1u << 24))
                 o2 = u32x4{(uint32_t)(nx - fi.frame_off),
-                           st_crc16_ok<2>((const uint8_t *)words, fi.frame_off, nx, cp.z, (uint64_t)cp.wc * 64u) ? 1u : 0u,
+                           st_crc16_ok<2>((const uint8_t *)words, fi.frame_off, nx, z, (uint64_t)cp.wc * 64u) ? 1u : 0u,
                            (uint32_t)fi.frame_off, 0u};
         }
         *(u32x4 *)(crcp + CRCP_WORDS * (uint64_t)f) = o;
@@ -2063,7 +2116,7 @@ DEV void crc_tk_fill(lds_u16 *TK, uint32_t lane) {
 /* ============================================================== k_parse
  * One lane per frame (parse_frame: the lane-serial subframe walk), 64 frames per single-wave
  * workgroup, in the parse order when there is one. */
-template <int CPM>
+template <int CPM, bool Y>
 __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint64_t nbytes,
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
@@ -2071,7 +2124,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
                                               const uint32_t *__restrict__ perm, uint32_t *__restrict__ crcp) {
     __shared__ LDS_DMA_ALIGN uint32_t ring[PARSE_RD * RING_LANE_DW]; /* the bit ring */
     const uint32_t slot = blockIdx.x * 64u + threadIdx.x; /* parse order (launch_order<1>) */
-    parse_frame<CPM>(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
+    parse_frame<CPM, Y>(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
                 (perm && slot < nframes) ? perm[slot] : slot, crcp);
 }
 
@@ -5086,15 +5139,23 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
     }
     if (cm == 3) cm = 1;
     if (handed) *handed = cm != 0;
-    if (cm == 2)
-        hipLaunchKernelGGL(k_parse<2>, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
-                           out_sample_in, base_sample, info, ablate_flags(), perm, crcp);
+    const dim3 g((nframes + 63) / 64);
+    const bool y = sp.bps <= 16u; /* the prefix's form (CrcPT) */
+    if (cm == 2 && y)
+        hipLaunchKernelGGL((k_parse<2, true>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
+                           base_sample, info, ablate_flags(), perm, crcp);
+    else if (cm == 2)
+        hipLaunchKernelGGL((k_parse<2, false>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
+                           base_sample, info, ablate_flags(), perm, crcp);
+    else if (cm == 1 && y)
+        hipLaunchKernelGGL((k_parse<1, true>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
+                           base_sample, info, ablate_flags(), perm, crcp);
     else if (cm == 1)
-        hipLaunchKernelGGL(k_parse<1>, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
-                           out_sample_in, base_sample, info, ablate_flags(), perm, crcp);
+        hipLaunchKernelGGL((k_parse<1, false>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
+                           base_sample, info, ablate_flags(), perm, crcp);
     else
-        hipLaunchKernelGGL(k_parse<0>, dim3((nframes + 63) / 64), dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp,
-                           out_sample_in, base_sample, info, ablate_flags(), perm, nullptr);
+        hipLaunchKernelGGL((k_parse<0, false>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
+                           base_sample, info, ablate_flags(), perm, nullptr);
     return hipGetLastError();
 }
 
