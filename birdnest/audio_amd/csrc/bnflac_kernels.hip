@@ -803,39 +803,27 @@ DEV void crcz_blk(CrcZ &c, uint4 v) {
  * one 16-byte block at a time (three live state words: k_parse's occupancy is LDS-bound at 5
  * waves per SIMD, ~100 VGPRs), and the decode tail continues from there, re-reading only the
  * rest of the frame. */
-/* The prefix state, two forms (k_parse<CPM, Y>):
- *  - Y (16-bit streams): the remainder mod Q(y) = y^15 + y + 1, y = x^32, in 15 words.
- *    Q(y) = T(x^32) = T(x)^32 is a multiple of T, so it keeps M mod T; with whole words as
- *    the coefficients a 64-byte line is 18 word XORs at once (S y^16 + sum W[i] y^(15-i):
- *    y^15 = y + 1, y^16 = y^2 + y; checked against bit-serial division mod T in Python while
- *    writing this) against 96 VALU through the T^4 form, and the words are taken as loaded
- *    (little-endian): a byte swap permutes the bits of every word alike, so it is applied to
- *    the 15 state words once, at the hand-off (crcp_z).  The state costs k_parse 128 VGPRs (4
- *    waves per SIMD): C2's bulk walk gains (k_parse 2.52 -> 2.16 ms against 1.95 without the
- *    prefix), while C3's plain walk lost with it (1.68 -> 2.18 ms on a build at 146 VGPRs,
- *    3 waves), hence
- *  - !Y (above 16 bits): the T^4 form of the decode tails (CrcZ, 3 words; 94 VGPRs, 5 waves). */
-template <bool Y> struct CrcPT;
-template <> struct CrcPT<true> {
+/* The prefix state: the remainder mod Q(y) = y^15 + y + 1, y = x^32, in 15 words.  Q(y) =
+ * T(x^32) = T(x)^32 is a multiple of T, so it keeps M mod T; with whole words as the
+ * coefficients a 64-byte line is 18 word XORs at once (S y^16 + sum W[i] y^(15-i): y^15 = y + 1,
+ * y^16 = y^2 + y; checked against bit-serial division mod T in Python while writing this)
+ * against 96 VALU through the T^4 form, and the words are taken as loaded (little-endian): a
+ * byte swap permutes the bits of every word alike, so it is applied to the 15 state words
+ * once, at the hand-off (crcp_z).  k_parse<1> 128 VGPRs, 4 waves per SIMD: C2 k_parse 2.52 ->
+ * 2.16 ms against the T^4 form (1.95 without a prefix), C3 the same as with it (10.43 vs
+ * 10.47 ms per step; a build at 146 VGPRs, 3 waves, had cost C3's plain walk 0.5 ms). */
+struct CrcP {
     uint32_t s[15]; /* s[k]: the coefficient of y^k (little-endian words) */
     uint32_t px;    /* XOR of every word (parity) */
     uint32_t wc;    /* next line to fold (absolute 64-byte line index); ~0: no prefix for this frame */
 };
-template <> struct CrcPT<false> {
-    CrcZ z;      /* remainder mod T^4 and parity */
-    uint32_t wc;
-};
-DEV void crcp_init(CrcPT<true> &c) {
+DEV void crcp_init(CrcP &c) {
 #pragma unroll
     for (int k = 0; k < 15; k++) c.s[k] = 0u;
     c.px = 0u;
     c.wc = ~0u;
 }
-DEV void crcp_init(CrcPT<false> &c) {
-    c.z = CrcZ{0u, 0u, 0u};
-    c.wc = ~0u;
-}
-DEV void crcp_fold(CrcPT<true> &c, const u32x4 (&v)[4]) {
+DEV void crcp_fold(CrcP &c, const u32x4 (&v)[4]) {
     const uint32_t W[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
                             v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
     c.px ^= W[0] ^ W[1] ^ W[2] ^ W[3] ^ W[4] ^ W[5] ^ W[6] ^ W[7] ^ W[8] ^ W[9] ^ W[10] ^ W[11] ^ W[12] ^ W[13] ^
@@ -849,20 +837,14 @@ DEV void crcp_fold(CrcPT<true> &c, const u32x4 (&v)[4]) {
     c.s[0] = r0;
     c.wc++;
 }
-DEV void crcp_fold(CrcPT<false> &c, const u32x4 (&v)[4]) {
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) crcz_blk(c.z, make_uint4(v[i].x, v[i].y, v[i].z, v[i].w));
-    c.wc++;
-}
 /* the remainder in the decode tails' T^4 form (st_crc16_ok continues it) */
-DEV CrcZ crcp_z(const CrcPT<true> &c) {
+DEV CrcZ crcp_z(const CrcP &c) {
     CrcZ z{0u, 0u, 0u};
 #pragma unroll
     for (int k = 14; k >= 0; k--) crcz_w(z, c.s[k]);
     z.px = c.px;
     return z;
 }
-DEV CrcZ crcp_z(const CrcPT<false> &c) { return c.z; }
 /* fold the lines before line cl (whole wave).  The ring holds the two lines [iend / 4 - 2,
  * iend / 4), and the refill keeps the line of word wi (the reader's next word) and the one
  * after it: so before a refill, cl = wi / 16 -- every line the reader has loaded, which the
@@ -1681,7 +1663,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_sync_write(const uint8_t *__re
 static_assert(PARSE_RD == 8, "pk_ra and the walk's pair steps (slot masks 0x3F3 / 0x1C0C, slot bits 10-12) assume an 8-slot ring");
 /* One lane per candidate frame: header + cursor walk over subframes 0..C-2.  Also
  * flags frames with an LPC order above 8 (they go to k_decode<32>). */
-template <int CPM, bool Y> /* the CRC-16 hand-off (crc_mode): 1 the prefix, 2 the prefix and the verdict; Y: its form (CrcPT) */
+template <int CPM> /* the CRC-16 hand-off (crc_mode): 1 the prefix, 2 the prefix and the verdict */
 DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const uint64_t *__restrict__ frame_offs,
                      uint32_t nframes, const bnf_stream_params &sp, const uint64_t *__restrict__ out_sample_in,
                      uint64_t base_sample, bnf_frame_info *__restrict__ info, uint32_t ablate, lds_u32 *ring,
@@ -1710,7 +1692,7 @@ DEV void parse_frame(const uint32_t *__restrict__ words, uint64_t nbytes, const 
     const uint64_t fbit = fi.frame_off * 8u;
     BR b;
     br_init(b, words, nbytes, ring, threadIdx.x, PARSE_RD);
-    CrcPT<Y> cp; /* the CRC-16 prefix of a 2-channel frame (crcp != nullptr: the batch decode's hand-off) */
+    CrcP cp; /* the CRC-16 prefix of a 2-channel frame (crcp != nullptr: the batch decode's hand-off) */
     crcp_init(cp);
     uint32_t st = parse_header(b, fbit, limit, sp, fi);
     if (st == BNF_ST_ERROR && br_pos(b) > limit) st = BNF_ST_TRUNC;
@@ -2116,7 +2098,7 @@ DEV void crc_tk_fill(lds_u16 *TK, uint32_t lane) {
 /* ============================================================== k_parse
  * One lane per frame (parse_frame: the lane-serial subframe walk), 64 frames per single-wave
  * workgroup, in the parse order when there is one. */
-template <int CPM, bool Y>
+template <int CPM>
 __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words, uint64_t nbytes,
                                               const uint64_t *__restrict__ frame_offs, uint32_t nframes,
                                               bnf_stream_params sp, const uint64_t *__restrict__ out_sample_in,
@@ -2124,7 +2106,7 @@ __global__ void __launch_bounds__(64) k_parse(const uint32_t *__restrict__ words
                                               const uint32_t *__restrict__ perm, uint32_t *__restrict__ crcp) {
     __shared__ LDS_DMA_ALIGN uint32_t ring[PARSE_RD * RING_LANE_DW]; /* the bit ring */
     const uint32_t slot = blockIdx.x * 64u + threadIdx.x; /* parse order (launch_order<1>) */
-    parse_frame<CPM, Y>(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
+    parse_frame<CPM>(words, nbytes, frame_offs, nframes, sp, out_sample_in, base_sample, info, ablate, (lds_u32 *)ring,
                 (perm && slot < nframes) ? perm[slot] : slot, crcp);
 }
 
@@ -5140,21 +5122,14 @@ hipError_t bnf_launch_parse(const uint32_t *words, uint64_t nbytes, const uint64
     if (cm == 3) cm = 1;
     if (handed) *handed = cm != 0;
     const dim3 g((nframes + 63) / 64);
-    const bool y = sp.bps <= 16u; /* the prefix's form (CrcPT) */
-    if (cm == 2 && y)
-        hipLaunchKernelGGL((k_parse<2, true>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
-                           base_sample, info, ablate_flags(), perm, crcp);
-    else if (cm == 2)
-        hipLaunchKernelGGL((k_parse<2, false>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
-                           base_sample, info, ablate_flags(), perm, crcp);
-    else if (cm == 1 && y)
-        hipLaunchKernelGGL((k_parse<1, true>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
+    if (cm == 2)
+        hipLaunchKernelGGL(k_parse<2>, g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
                            base_sample, info, ablate_flags(), perm, crcp);
     else if (cm == 1)
-        hipLaunchKernelGGL((k_parse<1, false>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
+        hipLaunchKernelGGL(k_parse<1>, g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
                            base_sample, info, ablate_flags(), perm, crcp);
     else
-        hipLaunchKernelGGL((k_parse<0, false>), g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
+        hipLaunchKernelGGL(k_parse<0>, g, dim3(64), 0, s, words, nbytes, frame_offs, nframes, sp, out_sample_in,
                            base_sample, info, ablate_flags(), perm, nullptr);
     return hipGetLastError();
 }
