@@ -40,7 +40,7 @@
 
 #define DEV __device__ __forceinline__
 
-/* ------------------------------------------------------------------ CRC tables */
+/* ------------------------------------------- CRC tables (CRC-8; slice-by-8 CRC-16 for k_decode<W>, k_decode_sys) */
 /* Tables are filled by the host at module load (bnflac_runtime.cpp) into these: */
 __constant__ uint8_t g_crc8_tab[256];
 __constant__ uint16_t g_crc16_tab[8][256]; /* slice-by-8 */
@@ -4023,11 +4023,12 @@ __global__ void __launch_bounds__(64, 2) k_decode_st(const uint32_t *__restrict_
     }
     /* CRC-16 of the frame bytes (read_frame_'s footer check @0x10011a01), by the table-free
      * zero test over frame + footer (st_crc16_ok; round 6: 10.8 -> 10.5 ms on C2 against round
-     * 5's 11-bit LDS tables, same box).  The tail is bound by the re-read: every wave of a CU
-     * reaches it together, so the 11 GB go at the HBM rate with no decode beside them (no CRC at
-     * all: 8.6 ms).  Keeping the remainder running inside the chunk loop instead (one line per
-     * refill point through the staging tile) needs ~6 more live VGPRs; at the 256 already in use
-     * the loop spilled (20-89 VGPRs) and the launch took 20 ms: dropped. */
+     * 5's 11-bit LDS tables, same box), continuing k_parse's prefix of the lines before channel
+     * 1 when the batch has one (st_crc16_frame: 10.7 -> 9.6 ms).  The tail is bound by the
+     * re-read: every wave of a CU reaches it together, so those bytes go at the HBM rate with no
+     * decode beside them (no CRC at all: ~8.6 ms).  Keeping the remainder running inside the
+     * chunk loop instead needs live VGPRs the loop does not have at 256: it spilled (11-89
+     * VGPRs in two attempts) and ran 30% slower with the fold off. */
     uint32_t crc = crc_read;
     if (ok && !(ablate & 1u) && !st_crc16_frame((const uint8_t *)words, crcp, f, fi.frame_off, end_byte + 2u)) ok = false;
     if (ok && crc != crc_read) ok = false;
@@ -4441,7 +4442,7 @@ __global__ void __launch_bounds__(64, 2) k_decode_sw(const uint32_t *__restrict_
     uint32_t trunc = 0;
     const bool sto = !(ablate & 2u);
     /* FILEREADER runs that start on a 64-byte line: the fused chunks flush whole lines
-     * (sw_line_flush); the slots sit past the two rings (the CRC tables' extra 4 KB).
+     * (sw_line_flush); the slots sit past the two rings (the 4 KB staging tile).
      * Ablation bit 0x20000000 (exact): per-lane 16-byte stores instead */
     const bool line = FMT == BNF_OUT_FILEREADER && sto && !hot && all_al && !(ablate & 0x20000000u) &&
                       !any_lane(ok && (((uintptr_t)dst) & 63u) != 0);
