@@ -114,6 +114,13 @@ DEV void gst128(uint64_t addr, u32x4 v) { *(__attribute__((address_space(1))) u3
 #define BNF_MODE_LIST 0x20000u
 /* Mode bit: k_decode_seg -- the W = 32 instance also takes the W16 class's blocks. */
 #define BNF_MODE_SEG 0x80000000u
+/* Mode bits of the W = 8 instance when its two jobs run as two launches (bnf_launch_decode):
+ * NOST -- the narrow non-stereo frames only (the decode order's class 1; beside k_decode_st,
+ * so it never reads a stereo frame's hand-back bit); STREDO -- only the stereo frames
+ * k_decode_st handed back (class 0; after it). */
+#define BNF_MODE_NOST 0x40000u
+#define BNF_MODE_STREDO 0x80000u
+#define BNF_ABLATE_NO_W8SPLIT 0x100000u /* host A/B bit: the W = 8 instance as one launch */
 
 /* ----------------------------------------------------------------- bit reader */
 #define RING_MAX 16       /* 16-byte slots per lane (k_parse and k_decode_st use 8) */
@@ -2555,7 +2562,8 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
         bool w = false;
         if (have && info[f].status == BNF_ST_OK) {
             const uint32_t fl = info[f].flags;
-            w = ((fl & BNF_FL_ST) && !(ablate & 0x400u)) ? (fl & BNF_FL_REDO) != 0 : !(fl & (BNF_FL_W16 | BNF_FL_W32));
+            if ((fl & BNF_FL_ST) && !(ablate & 0x400u)) w = !(ablate & BNF_MODE_NOST) && (fl & BNF_FL_REDO) != 0;
+            else w = !(ablate & BNF_MODE_STREDO) && !(fl & (BNF_FL_W16 | BNF_FL_W32));
         }
         if (!__any(w)) return;
     }
@@ -2565,7 +2573,8 @@ DEV void decode_block(uint32_t blk, uint32_t *ring, int32_t *lds, const uint32_t
      * The W = 16 and 32 instances run beside them on a second stream and never look at
      * ST frames (the ST bit is k_parse's and does not change; REDO may be being set). */
     const bool st_frame = have && (fi.flags & BNF_FL_ST) && !(ablate & 0x400u) && !lst;
-    if (st_frame && (MAXW != 8 || !(fi.flags & BNF_FL_REDO))) have = false;
+    if (st_frame && (MAXW != 8 || (ablate & BNF_MODE_NOST) || !(fi.flags & BNF_FL_REDO))) have = false;
+    if (MAXW == 8 && (ablate & BNF_MODE_STREDO) && !st_frame) have = false;
     if (have && sw_on && (fi.flags & BNF_FL_SW) && !(fi.flags & BNF_FL_REDO)) have = false;
     bool frame_ok = have && fi.status == BNF_ST_OK;
     /* one wave per workgroup: the W = 8, 16 and 32 instances split the blocks between them
@@ -2946,10 +2955,10 @@ __global__ void __launch_bounds__(DEC_LANES, 2) k_decode(const uint32_t *__restr
                                                       const uint32_t *__restrict__ seg) {
     __shared__ LDS_DMA_ALIGN uint32_t ring[RD * RING_LANE_DW];
     __shared__ int32_t lds[CHK * RP]; /* [sample][lane] */
-    if (MAXW != 8 && seg) {
+    if (seg) { /* W = 8: only as one of its two launches (BNF_MODE_NOST / BNF_MODE_STREDO) */
         const uint32_t fpb = DEC_LANES >> __builtin_ctz(chn_lanes);
-        const uint32_t c = MAXW == 32 ? 3u : 2u; /* order_key's class */
-        const uint32_t lo = seg[c * 64u - 1u] / fpb, end = (seg[c * 64u + 63u] + fpb - 1u) / fpb;
+        const uint32_t c = MAXW == 32 ? 3u : MAXW == 16 ? 2u : (ablate & BNF_MODE_NOST) ? 1u : 0u; /* order_key's class */
+        const uint32_t lo = c ? seg[c * 64u - 1u] / fpb : 0u, end = (seg[c * 64u + 63u] + fpb - 1u) / fpb;
         if (blockIdx.x < lo || blockIdx.x >= end) return;
     }
     decode_block<MAXW, CHK, RD>(blockIdx.x, ring, lds, words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info,
@@ -4652,7 +4661,7 @@ hipError_t TU_FN(bnf_launch_decode)(const uint32_t *words, uint64_t nbytes, uint
                                     const uint32_t *perm, uint32_t mode, const uint32_t *seg, hipStream_t s) {
     const uint32_t fpb = DEC_LANES / chn_lanes;
     const uint32_t nb = (nframes + fpb - 1) / fpb;
-    if (DEC_W == 8 || !perm) seg = nullptr;
+    if (!perm || (DEC_W == 8 && !(mode & (BNF_MODE_NOST | BNF_MODE_STREDO)))) seg = nullptr;
     hipLaunchKernelGGL((k_decode<DEC_W, 32, DEC_RD>), dim3(nb), dim3(DEC_LANES), 0, s, words, nbytes, nframes, sp, chn_lanes,
                        fmt, out, out_bytes, info, perm, ablate_flags() | mode, seg);
     return hipGetLastError();
@@ -4927,6 +4936,7 @@ __global__ void __launch_bounds__(ORDER_NB) k_order_scan(uint32_t *__restrict__ 
         cls[0] = t[3u * 64u - 1u] - t[2u * 64u - 1u];
         cls[1] = t[4u * 64u - 1u] - t[3u * 64u - 1u];
         cls[2] = t[ORDER_NB - 1u]; /* every frame of the order */
+        cls[3] = t[2u * 64u - 1u] - t[64u - 1u]; /* class 1: narrow non-stereo frames (and failed ones) */
     }
 }
 template <int MODE>
@@ -4968,9 +4978,9 @@ static hipError_t launch_order(const bnf_frame_info *info, const uint8_t *bytes,
  * (created on first use, kept for the process), and the decode order
  * (BNFLAC_DECODE_SERIAL=1: every decode instance on the caller's stream). */
 struct SideQ {
-    hipStream_t st[2]; /* W16, W32 */
-    hipEvent_t fork, join[2];
-    uint32_t *cls; /* host memory: the last decode order's W16 / W32 class sizes and its frame count (k_order_scan) */
+    hipStream_t st[3]; /* W16, W32, the W8 instance's class-1 launch */
+    hipEvent_t fork, join[3];
+    uint32_t *cls; /* host memory: the last decode order's W16 / W32 class sizes, its frame count and its class 1 size (k_order_scan) */
 };
 static std::mutex g_side_mu;
 static std::atomic<uint64_t> g_seg_launches{0}; /* k_decode_seg launches (bnf_decode_seg_launches) */
@@ -4991,13 +5001,13 @@ static SideQ *side_queue() { /* under g_side_mu; nullptr: decode serially */
     if (!q.st[1]) {
         SideQ n = {};
         bool ok = hipEventCreateWithFlags(&n.fork, hipEventDisableTiming) == hipSuccess;
-        for (int i = 0; i < 2 && ok; i++)
+        for (int i = 0; i < 3 && ok; i++)
             ok = hipStreamCreateWithFlags(&n.st[i], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&n.join[i], hipEventDisableTiming) == hipSuccess;
         if (ok && hipHostMalloc((void **)&n.cls, 64, hipHostMallocCoherent) != hipSuccess) n.cls = nullptr;
-        if (n.cls) n.cls[0] = n.cls[1] = n.cls[2] = ~0u; /* unknown: the full grids */
+        if (n.cls) n.cls[0] = n.cls[1] = n.cls[2] = n.cls[3] = ~0u; /* unknown: the full grids */
         if (!ok) {
-            for (int i = 0; i < 2; i++) {
+            for (int i = 0; i < 3; i++) {
                 if (n.join[i]) (void)hipEventDestroy(n.join[i]);
                 if (n.st[i]) (void)hipStreamDestroy(n.st[i]);
             }
@@ -5043,14 +5053,21 @@ static bool use_decode_sys(uint32_t nframes, const bnf_stream_params &sp, uint32
         m = e ? (atoi(e) ? 1 : 0) : 2;
         g_decode_sys.store(m, std::memory_order_relaxed);
     }
-    (void)sp;
     if (chn_lanes > 8u || m == 0) return false;
     if (m == 1) return true;
     static const uint32_t lim = [] {
         const char *e = getenv("BNFLAC_SYS_WAVES");
         return e ? (uint32_t)strtoul(e, nullptr, 0) : SYS_AUTO_WAVES;
     }();
-    return (uint64_t)nframes * chn_lanes < (uint64_t)lim * 64u;
+    /* A variable-blocksize stream's lane waves last as long as its longest frames while most
+     * frames are short, so the lane kernels need that many more frames to pay: the limit
+     * scales with max_blocksize / 2048 (tools/sys_crossover.sh, profiles/r6_sys_crossover.txt:
+     * C4, blocksizes 192-16384, sys 5.2 / 10.7 / 15.6 / 20.4 ms against the lanes' 15.8 / 17.2 /
+     * 17.6 / 18.0 at 8 / 32 / 48 / 64 copies of 4,096 frames; C2 and C3, fixed blocksizes, cross
+     * between 16 and 32 copies of 1,024 frames, where the unscaled limit already is) */
+    uint64_t scale = 1;
+    if (sp.has_stream_info && sp.max_blocksize > sp.min_blocksize && sp.max_blocksize > 4096u) scale = sp.max_blocksize / 2048u;
+    return (uint64_t)nframes * chn_lanes < (uint64_t)lim * 64u * scale;
 }
 
 /* The CRC-16 hand-off (crcp, CRCP_WORDS): 0 none (the decode tails read every frame again),
@@ -5201,14 +5218,25 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
         sq = nullptr;
         lk.unlock();
     }
+    /* The W = 8 instance's two jobs as two launches when the previous decode order on this
+     * device had class-1 frames (narrow non-stereo: VERBATIM / CONSTANT subframes; C4): those
+     * on a third side stream beside k_decode_st, and after k_decode_st only its hand-backs.
+     * One launch after k_decode_st put both on the stream's critical path (C4 at 32 copies:
+     * k_decode_st 11.7 ms, then k_decode<8> 6.3 ms, while the W16 / W32 grids ended at 10.9). */
+    const bool w8split = sq && seg && cls && __atomic_load_n(&cls[3], __ATOMIC_RELAXED) != 0u &&
+                         !(ablate_flags() & BNF_ABLATE_NO_W8SPLIT);
+    const int nside = w8split ? 3 : 2;
     auto fork = [&]() -> hipError_t {
         hipError_t r = hipEventRecord(sq->fork, s);
-        for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipStreamWaitEvent(sq->st[i], sq->fork, 0);
+        for (int i = 0; i < nside && r == hipSuccess; i++) r = hipStreamWaitEvent(sq->st[i], sq->fork, 0);
         if (r == hipSuccess)
             r = bnf_launch_decode_tu2(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, sq->st[1]);
         if (r == hipSuccess)
             r = bnf_launch_decode_tu5(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, seg, sq->st[0]);
-        for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipEventRecord(sq->join[i], sq->st[i]);
+        if (r == hipSuccess && w8split)
+            r = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm,
+                                      mode | BNF_MODE_NOST, seg, sq->st[2]);
+        for (int i = 0; i < nside && r == hipSuccess; i++) r = hipEventRecord(sq->join[i], sq->st[i]);
         return r;
     };
     if (sq && fm == 2 && e == hipSuccess) e = fork();
@@ -5221,9 +5249,12 @@ hipError_t bnf_launch_decode(const uint32_t *words, uint64_t nbytes, uint32_t nf
                 ? bnf_launch_decode_tu3(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, crcp, s)
                 : bnf_launch_decode_tu4(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, crcp, s);
     if (sq && fm == 1 && e == hipSuccess) e = fork();
-    if (e == hipSuccess) e = bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, nullptr, s);
+    if (e == hipSuccess)
+        e = w8split ? bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm,
+                                            mode | BNF_MODE_STREDO, seg, s)
+                    : bnf_launch_decode_tu1(words, nbytes, nframes, sp, chn_lanes, fmt, out, out_bytes, info, perm, mode, nullptr, s);
     if (sq) {
-        for (int i = 0; i < 2; i++) { /* joined even if a launch failed */
+        for (int i = 0; i < nside; i++) { /* joined even if a launch failed */
             const hipError_t ej = hipStreamWaitEvent(s, sq->join[i], 0);
             if (e == hipSuccess) e = ej;
         }
