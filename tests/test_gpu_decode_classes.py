@@ -38,7 +38,7 @@ def _lane_kernels():
     L.bnflac_debug_set_decode_sys(-1)
 
 
-def _mixed_batch(n_each):
+def _mixed_batch(n_each, class1=False):
     from birdnest.audio_amd import synth
     parts = [
         synth.encode(synth.config("C2", nframes=n_each, stereo_mode=3, level=0.9, noise=0.5, seed=41)),
@@ -46,6 +46,9 @@ def _mixed_batch(n_each):
         synth.encode(synth.config("C2", nframes=n_each, order=32, partition_order=-1, seed=43)),
         synth.encode(synth.config("C2", nframes=n_each, seed=44)),
     ]
+    if class1:  # C4's subframe mix at a fixed blocksize: VERBATIM / CONSTANT frames (decode class 1)
+        parts.append(synth.encode(synth.config("C2", nframes=n_each, subframe_mode=synth.SUB_MIXED,
+                                               stereo_mode=synth.ST_CYCLE, partition_order=-1, seed=45)))
     data, offs, osmp, pcm = bytearray(), [], [], []
     base = 0
     for s in parts:
@@ -139,3 +142,25 @@ def test_segment_grid_after_batch_without_w16_w32(n_each):
     out2, info2 = _decode(data, offs, osmp, total)  # this batch had both: the side grids again
     assert L.bnflac_debug_decode_seg_launches() == n0 + 1
     assert out2.tobytes() == out.tobytes() and info2.tobytes() == info.tobytes()
+
+
+@pytest.mark.skipif(not gpu_available(), reason="no GPU")
+@pytest.mark.parametrize("n_each", [9, 40])
+def test_w8_split_launches(n_each):
+    """k_decode<8> as two launches (the class-1 frames on a third side stream beside
+    k_decode_st, the stereo hand-backs after it) once the previous decode order had class-1
+    frames: the same bytes and records as the single launch (host bit 0x100000)."""
+    from birdnest.audio_amd import libflac
+    L = libflac.load()
+    data, offs, osmp, pcm, total = _mixed_batch(n_each, class1=True)
+    _decode(data, offs, osmp, total)  # records the class-1 count for the next decode
+    out, info = _decode(data, offs, osmp, total)
+    assert (info["status"] == 0).all() and (info["crc_ok"] == 1).all()
+    assert (info["flags"] & FL_REDO).any(), "the batch should hold handed-back stereo frames"
+    assert np.array_equal(out.view("<i4").reshape(-1, 2), pcm)
+    L.bnflac_debug_set_ablate(0x100000)
+    try:
+        out1, info1 = _decode(data, offs, osmp, total)
+    finally:
+        L.bnflac_debug_set_ablate(0)
+    assert out1.tobytes() == out.tobytes() and info1.tobytes() == info.tobytes()
